@@ -1,0 +1,651 @@
+/*
+ * disort_oracle.c -- plain-C FP64 restatement of the flux-only DISORT solve.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Used by tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py, as the checker and as the timed CPU baseline
+ * ("port": a CPU restatement of cdisort, NOT cdisort).  Never linked into the
+ * product library (pyharp_amd/libhdisort.so).
+ *
+ * Reference: pyharp calls pydisort @ afee3ec897f (cmake/pydisort.cmake:9-11),
+ * which wraps cdisort 2.1.3 (src/rtsolver/rtsolver.hpp:16).  Neither is in the
+ * container, so this restates the published DISORT method with cdisort's stage
+ * structure (same as oracle/disort_np.py, which pins it):
+ *   c_qgausn   -> gauss_01()          Gauss-Legendre nodes on (0,1)
+ *   c_setdis   -> setdis part of solve_column()  (dither, delta-M)
+ *   c_soleig   -> soleig()            eigenproblem (alpha-beta)(alpha+beta), nstr/2
+ *                 (solved through its symmetric form, Cholesky + cyclic Jacobi,
+ *                 instead of ASYMTX's Hessenberg QR; eigenpairs are unique)
+ *   c_upbeam   -> dense nstr x nstr LU with partial pivoting (SGECO/SGESL)
+ *   c_upisot   -> two dense nstr x nstr solves
+ *   c_setmtx + c_solve0 -> banded matrix, half-bandwidth 3*nstr/2-1, banded LU
+ *                 with partial pivoting (LINPACK SGBFA/SGBSL algorithm)
+ *   c_fluxes   -> flux sums at the layer boundaries
+ *   c_planck_func1 -> plkavg() (DISORT PLKAVG series, same truncation)
+ * harp conventions (layer 0 = bottom in prop/temf/flux, F_dn = rfldir+rfldn)
+ * follow examples/amars_sw.cpp:141-146,185-191 and rt_solver_disort.cpp_:172-181.
+ *
+ * Parity status: parity unpinned against cdisort (absent).  Pinned by the
+ * DISOTEST problem-1 fluxes in tests/golden/disotest1.json and by agreement
+ * with oracle/disort_np.py (tests/test_oracle.py).
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include <float.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define MAXNN 32
+#define MAXN (2 * MAXNN)
+#define PI 3.14159265358979323846
+
+static const double PLK_C2 = 1.438786;
+static const double PLK_SIGMA = 5.67032e-8;
+static const double PLK_VCUT = 1.5;
+static const double PLK_VCP[7] = {10.25, 5.7, 3.9, 2.9, 2.3, 1.9, 0.0};
+
+/* ------------------------------------------------------------------------ */
+/* quadrature / Legendre                                                     */
+/* ------------------------------------------------------------------------ */
+static void gauss_01(int nn, double *mu, double *w) {
+  /* Newton iteration on P_nn(x) in (-1,1), mapped to (0,1) ascending. */
+  for (int i = 0; i < (nn + 1) / 2; ++i) {
+    double x = cos(PI * (i + 0.75) / (nn + 0.5));
+    double dp = 0.0;
+    for (int it = 0; it < 100; ++it) {
+      double p0 = 1.0, p1 = x;
+      for (int l = 2; l <= nn; ++l) {
+        double p2 = ((2 * l - 1) * x * p1 - (l - 1) * p0) / l;
+        p0 = p1;
+        p1 = p2;
+      }
+      if (nn == 1) { p1 = x; p0 = 1.0; }
+      dp = nn * (x * p1 - p0) / (x * x - 1.0);
+      double dx = p1 / dp;
+      x -= dx;
+      if (fabs(dx) < 1e-16) break;
+    }
+    {
+      double p0 = 1.0, p1 = x;
+      for (int l = 2; l <= nn; ++l) {
+        double p2 = ((2 * l - 1) * x * p1 - (l - 1) * p0) / l;
+        p0 = p1;
+        p1 = p2;
+      }
+      if (nn == 1) { p1 = x; p0 = 1.0; }
+      dp = nn * (x * p1 - p0) / (x * x - 1.0);
+    }
+    double wx = 2.0 / ((1.0 - x * x) * dp * dp);
+    /* x is the i-th largest root; nodes +x and -x */
+    mu[nn - 1 - i] = 0.5 * (1.0 + x);
+    w[nn - 1 - i] = 0.5 * wx;
+    mu[i] = 0.5 * (1.0 - x);
+    w[i] = 0.5 * wx;
+  }
+}
+
+static void legendre(int lmax, double x, double *p) {
+  p[0] = 1.0;
+  if (lmax > 1) p[1] = x;
+  for (int l = 2; l < lmax; ++l)
+    p[l] = ((2 * l - 1) * x * p[l - 1] - (l - 1) * p[l - 2]) / l;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Planck (DISORT PLKAVG restated)                                           */
+/* ------------------------------------------------------------------------ */
+static double plkf(double x) { return x * x * x / expm1(x); }
+
+double hdo_plkavg(double wnumlo, double wnumhi, double t) {
+  if (t < 0.0 || wnumhi <= wnumlo || wnumlo < 0.0) return NAN;
+  if (t < 1.0e-4) return 0.0;
+  const double sigdpi = PLK_SIGMA / PI;
+  const double conc = 15.0 / (PI * PI * PI * PI);
+  double v[2] = {PLK_C2 * wnumlo / t, PLK_C2 * wnumhi / t};
+  const double vmax = log(DBL_MAX), epsil = DBL_EPSILON;
+  if (v[0] > epsil && v[1] < vmax && (wnumhi - wnumlo) / wnumhi < 1.0e-2) {
+    double hh = v[1] - v[0], oldval = 0.0, val0 = plkf(v[0]) + plkf(v[1]), val = 0.0;
+    for (int n = 1; n <= 10; ++n) {
+      double del = hh / (2 * n);
+      val = val0;
+      for (int k = 1; k <= 2 * n - 1; ++k) val += 2 * (1 + k % 2) * plkf(v[0] + k * del);
+      val = del / 3.0 * val;
+      if (fabs((val - oldval) / val) <= 1.0e-6) break;
+      oldval = val;
+    }
+    return sigdpi * t * t * t * t * conc * val;
+  }
+  const double a1 = 1.0 / 3.0, a2 = -1.0 / 8.0, a3 = 1.0 / 60.0, a4 = -1.0 / 5040.0,
+               a5 = 1.0 / 272160.0, a6 = -1.0 / 13305600.0, a7 = 1.0 / 622702080.0;
+  double p[2] = {0, 0}, d[2] = {0, 0};
+  int smallv = 0;
+  for (int i = 0; i < 2; ++i) {
+    double vi = v[i];
+    if (vi < PLK_VCUT) {
+      smallv++;
+      double vsq = vi * vi;
+      p[i] = conc * vsq * vi *
+             (a1 + vi * (a2 + vi * (a3 + vsq * (a4 + vsq * (a5 + vsq * (a6 + vsq * a7))))));
+    } else {
+      int mmax = 0;
+      do { mmax++; } while (vi < PLK_VCP[mmax - 1]);
+      double ex = exp(-vi), exm = 1.0, di = 0.0;
+      for (int m = 1; m <= mmax; ++m) {
+        double mv = m * vi;
+        exm *= ex;
+        di += exm * (6.0 + mv * (6.0 + mv * (3.0 + mv))) / ((double)m * m * m * m);
+      }
+      d[i] = conc * di;
+    }
+  }
+  double val;
+  if (smallv == 2) val = p[1] - p[0];
+  else if (smallv == 1) val = 1.0 - p[0] - d[1];
+  else val = d[0] - d[1];
+  return sigdpi * t * t * t * t * val;
+}
+
+/* ------------------------------------------------------------------------ */
+/* small dense linear algebra                                                */
+/* ------------------------------------------------------------------------ */
+/* LU with partial pivoting, a is n x n row-major (lda = n). returns 0/1 */
+static int lu_factor(int n, double *a, int *piv) {
+  int sing = 0;
+  for (int k = 0; k < n; ++k) {
+    int p = k;
+    double amax = fabs(a[k * n + k]);
+    for (int i = k + 1; i < n; ++i)
+      if (fabs(a[i * n + k]) > amax) { amax = fabs(a[i * n + k]); p = i; }
+    piv[k] = p;
+    if (amax == 0.0) { sing = 1; continue; }
+    if (p != k)
+      for (int j = 0; j < n; ++j) { double t = a[k * n + j]; a[k * n + j] = a[p * n + j]; a[p * n + j] = t; }
+    double inv = 1.0 / a[k * n + k];
+    for (int i = k + 1; i < n; ++i) {
+      double l = a[i * n + k] * inv;
+      a[i * n + k] = l;
+      if (l != 0.0)
+        for (int j = k + 1; j < n; ++j) a[i * n + j] -= l * a[k * n + j];
+    }
+  }
+  return sing;
+}
+
+static void lu_solve(int n, const double *a, const int *piv, double *b) {
+  /* rows were swapped whole (LAPACK getrf style): permute b first */
+  for (int k = 0; k < n; ++k) {
+    int p = piv[k];
+    if (p != k) { double t = b[k]; b[k] = b[p]; b[p] = t; }
+  }
+  for (int k = 0; k < n; ++k)
+    for (int i = k + 1; i < n; ++i) b[i] -= a[i * n + k] * b[k];
+  for (int k = n - 1; k >= 0; --k) {
+    b[k] /= a[k * n + k];
+    for (int i = 0; i < k; ++i) b[i] -= a[i * n + k] * b[k];
+  }
+}
+
+/* Cholesky a = L L^T, L lower (row-major, n x n). */
+static int cholesky(int n, const double *a, double *l) {
+  memset(l, 0, sizeof(double) * n * n);
+  for (int j = 0; j < n; ++j) {
+    double s = a[j * n + j];
+    for (int k = 0; k < j; ++k) s -= l[j * n + k] * l[j * n + k];
+    if (!(s > 0.0)) return 1;
+    double d = sqrt(s);
+    l[j * n + j] = d;
+    for (int i = j + 1; i < n; ++i) {
+      double t = a[i * n + j];
+      for (int k = 0; k < j; ++k) t -= l[i * n + k] * l[j * n + k];
+      l[i * n + j] = t / d;
+    }
+  }
+  return 0;
+}
+
+/* cyclic Jacobi on symmetric a (destroyed); eigenvalues -> ev, vectors -> v cols */
+static void jacobi(int n, double *a, double *ev, double *v) {
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) v[i * n + j] = (i == j);
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    double off = 0.0, tot = 0.0;
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j) {
+        double q = a[i * n + j] * a[i * n + j];
+        tot += q;
+        if (i != j) off += q;
+      }
+    if (off <= 1e-34 * tot || off == 0.0) break;
+    for (int p = 0; p < n - 1; ++p)
+      for (int q = p + 1; q < n; ++q) {
+        double apq = a[p * n + q];
+        if (apq == 0.0) continue;
+        double d = a[q * n + q] - a[p * n + p];
+        double t = 2.0 * apq / (fabs(d) + sqrt(d * d + 4.0 * apq * apq));
+        if (d < 0.0) t = -t;
+        double c = 1.0 / sqrt(1.0 + t * t), s = t * c;
+        for (int k = 0; k < n; ++k) { /* columns p,q */
+          double akp = a[k * n + p], akq = a[k * n + q];
+          a[k * n + p] = c * akp - s * akq;
+          a[k * n + q] = s * akp + c * akq;
+        }
+        for (int k = 0; k < n; ++k) { /* rows p,q */
+          double apk = a[p * n + k], aqk = a[q * n + k];
+          a[p * n + k] = c * apk - s * aqk;
+          a[q * n + k] = s * apk + c * aqk;
+        }
+        for (int k = 0; k < n; ++k) {
+          double vkp = v[k * n + p], vkq = v[k * n + q];
+          v[k * n + p] = c * vkp - s * vkq;
+          v[k * n + q] = s * vkp + c * vkq;
+        }
+      }
+  }
+  for (int i = 0; i < n; ++i) ev[i] = a[i * n + i];
+}
+
+/* ------------------------------------------------------------------------ */
+/* banded LU with partial pivoting (LINPACK SGBFA / SGBSL algorithm)         */
+/* storage: element (i,j) at ab[j*ld + kv + i - j], kv = kl+ku, ld = 2kl+ku+1 */
+/* ------------------------------------------------------------------------ */
+static int gb_factor(int n, int kl, int ku, double *ab, int ld, int *piv) {
+  const int kv = kl + ku;
+  int ju = 0, info = 0;
+  for (int j = 0; j < n; ++j) {
+    int km = kl < n - 1 - j ? kl : n - 1 - j;
+    int jp = 0;
+    double amax = fabs(ab[j * ld + kv]);
+    for (int i = 1; i <= km; ++i)
+      if (fabs(ab[j * ld + kv + i]) > amax) { amax = fabs(ab[j * ld + kv + i]); jp = i; }
+    piv[j] = j + jp;
+    if (amax == 0.0) { info = j + 1; continue; }
+    int jlim = j + ku + jp;
+    if (jlim > n - 1) jlim = n - 1;
+    if (jlim > ju) ju = jlim;
+    if (jp != 0)
+      for (int c = j; c <= ju; ++c) {
+        double *x = &ab[c * ld + kv + j - c], *y = &ab[c * ld + kv + j + jp - c];
+        double t = *x; *x = *y; *y = t;
+      }
+    double inv = 1.0 / ab[j * ld + kv];
+    for (int i = 1; i <= km; ++i) ab[j * ld + kv + i] *= inv;
+    for (int c = j + 1; c <= ju; ++c) {
+      double f = ab[c * ld + kv + j - c];
+      if (f != 0.0)
+        for (int i = 1; i <= km; ++i) ab[c * ld + kv + j + i - c] -= f * ab[j * ld + kv + i];
+    }
+  }
+  return info;
+}
+
+static void gb_solve(int n, int kl, int ku, const double *ab, int ld, const int *piv, double *b) {
+  const int kv = kl + ku;
+  for (int j = 0; j < n - 1; ++j) {
+    int km = kl < n - 1 - j ? kl : n - 1 - j;
+    int l = piv[j];
+    if (l != j) { double t = b[l]; b[l] = b[j]; b[j] = t; }
+    for (int i = 1; i <= km; ++i) b[j + i] -= ab[j * ld + kv + i] * b[j];
+  }
+  for (int j = n - 1; j >= 0; --j) {
+    b[j] /= ab[j * ld + kv];
+    int lm = kv < j ? kv : j;
+    for (int i = 1; i <= lm; ++i) b[j - i] -= ab[j * ld + kv - i] * b[j];
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* one column solve (cdisort conventions: layers top->bottom)                */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  int nstr, nlyr, nmom, planck;
+  const double *dtauc, *ssalb, *pmom; /* pmom: nlyr x (nmom+1), pmom[l][0]=1 */
+  const double *temper;               /* nlyr+1, top->bottom (planck)       */
+  double umu0, fbeam, albedo, fisot, btemp, ttemp, temis, wvnmlo, wvnmhi;
+} hdo_column_in;
+
+typedef struct {
+  double *work;
+  size_t nwork;
+  int *iwork;
+  size_t niwork;
+} hdo_ws;
+
+static double *ws_d(hdo_ws *ws, size_t n) {
+  if (ws->nwork < n) { free(ws->work); ws->work = (double *)malloc(n * sizeof(double)); ws->nwork = n; }
+  return ws->work;
+}
+static int *ws_i(hdo_ws *ws, size_t n) {
+  if (ws->niwork < n) { free(ws->iwork); ws->iwork = (int *)malloc(n * sizeof(int)); ws->niwork = n; }
+  return ws->iwork;
+}
+
+/* returns 0 ok, >0 numerical failure.  out arrays are nlyr+1 top->bottom */
+static int solve_column(const hdo_column_in *in, double *rfldir, double *rfldn, double *flup,
+                        hdo_ws *ws) {
+  const int nstr = in->nstr, nn = nstr / 2, nlyr = in->nlyr;
+  const double dither = sqrt(10.0 * DBL_EPSILON);
+  double cmu[MAXNN], cwt[MAXNN], cmuf[MAXN], cwtf[MAXN];
+  double ylm[MAXN][MAXN]; /* ylm[l][i] = P_l(cmuf_i) */
+  if (nstr < 2 || nstr % 2 || nn > MAXNN) return 1;
+  gauss_01(nn, cmu, cwt);
+  for (int i = 0; i < nn; ++i) {
+    cmuf[i] = cmu[i]; cmuf[nn + i] = -cmu[i];
+    cwtf[i] = cwt[i]; cwtf[nn + i] = cwt[i];
+  }
+  for (int i = 0; i < nstr; ++i) {
+    double p[MAXN];
+    legendre(nstr, cmuf[i], p);
+    for (int l = 0; l < nstr; ++l) ylm[l][i] = p[l];
+  }
+  const int beam = in->fbeam > 0.0 && in->umu0 > 0.0;
+
+  /* workspace layout */
+  const int ncol = nstr * nlyr, bw = 3 * nn - 1, ld = 3 * bw + 1;
+  size_t need = (size_t)nlyr * (nn + nstr * nstr + 3 * nstr + 3) + 3 * (nlyr + 1) +
+                (size_t)ld * ncol + ncol;
+  double *base = ws_d(ws, need);
+  double *kk = base;                        /* nlyr*nn        */
+  double *gc = kk + nlyr * nn;              /* nlyr*nstr*nstr */
+  double *zb = gc + (size_t)nlyr * nstr * nstr; /* nlyr*nstr   */
+  double *z0 = zb + nlyr * nstr;
+  double *z1 = z0 + nlyr * nstr;
+  double *dtaucp = z1 + nlyr * nstr;        /* nlyr */
+  double *oprim = dtaucp + nlyr;            /* nlyr */
+  double *ee_unused = oprim + nlyr;         /* nlyr */
+  double *taucpr = ee_unused + nlyr;        /* nlyr+1 */
+  double *tauc = taucpr + nlyr + 1;         /* nlyr+1 */
+  double *pkag = tauc + nlyr + 1;           /* nlyr+1 */
+  double *ab = pkag + nlyr + 1;             /* ld*ncol */
+  double *rhs = ab + (size_t)ld * ncol;     /* ncol */
+  int *ipiv = ws_i(ws, ncol);
+  (void)ee_unused;
+
+  taucpr[0] = tauc[0] = 0.0;
+  for (int lc = 0; lc < nlyr; ++lc) {
+    double ssa = in->ssalb[lc];
+    if (ssa == 1.0) ssa = 1.0 - dither;
+    const double *pm = in->pmom + (size_t)lc * (in->nmom + 1);
+    double f = in->nmom >= nstr ? pm[nstr] : 0.0;
+    dtaucp[lc] = (1.0 - ssa * f) * in->dtauc[lc];
+    oprim[lc] = ssa * (1.0 - f) / (1.0 - ssa * f);
+    taucpr[lc + 1] = taucpr[lc] + dtaucp[lc];
+    tauc[lc + 1] = tauc[lc] + in->dtauc[lc];
+  }
+  double bplanck = 0.0, tplanck = 0.0;
+  for (int l = 0; l <= nlyr; ++l) pkag[l] = 0.0;
+  if (in->planck) {
+    for (int l = 0; l <= nlyr; ++l) pkag[l] = hdo_plkavg(in->wvnmlo, in->wvnmhi, in->temper[l]);
+    bplanck = hdo_plkavg(in->wvnmlo, in->wvnmhi, in->btemp);
+    tplanck = hdo_plkavg(in->wvnmlo, in->wvnmhi, in->ttemp) * in->temis;
+  }
+  double p0[MAXN];
+  if (beam) legendre(nstr, -in->umu0, p0);
+
+  /* ---- per-layer: soleig, upbeam, upisot ---- */
+  for (int lc = 0; lc < nlyr; ++lc) {
+    double ssa = in->ssalb[lc];
+    if (ssa == 1.0) ssa = 1.0 - dither;
+    const double *pm = in->pmom + (size_t)lc * (in->nmom + 1);
+    double f = in->nmom >= nstr ? pm[nstr] : 0.0;
+    double gl[MAXN];
+    for (int k = 0; k < nstr; ++k) {
+      double chi = k <= in->nmom ? pm[k] : 0.0;
+      gl[k] = (2 * k + 1) * oprim[lc] * (chi - f) / (1.0 - f);
+    }
+    (void)ssa;
+    static __thread double cc[MAXN * MAXN];
+    for (int i = 0; i < nstr; ++i)
+      for (int j = 0; j < nstr; ++j) {
+        double s = 0.0;
+        for (int l = 0; l < nstr; ++l) s += gl[l] * ylm[l][i] * ylm[l][j];
+        cc[i * nstr + j] = 0.5 * s * cwtf[j];
+      }
+    /* soleig: eig of (alpha-beta)(alpha+beta) via its symmetric form */
+    double am[MAXNN * MAXNN], ap[MAXNN * MAXNN], lch[MAXNN * MAXNN], sym[MAXNN * MAXNN],
+        v[MAXNN * MAXNN], k2[MAXNN], sd[MAXNN];
+    for (int i = 0; i < nn; ++i) sd[i] = sqrt(cwt[i] / cmu[i]);
+    for (int i = 0; i < nn; ++i)
+      for (int j = 0; j < nn; ++j) {
+        /* S+ = (CC++ + CC+-)/w_j, S- = (CC++ - CC+-)/w_j */
+        double spp = (cc[i * nstr + j] + cc[i * nstr + nn + j]) / cwt[j];
+        double smm = (cc[i * nstr + j] - cc[i * nstr + nn + j]) / cwt[j];
+        am[i * nn + j] = (i == j ? 1.0 / cmu[i] : 0.0) - sd[i] * smm * sd[j];
+        ap[i * nn + j] = (i == j ? 1.0 / cmu[i] : 0.0) - sd[i] * spp * sd[j];
+      }
+    if (cholesky(nn, am, lch)) return 2;
+    for (int i = 0; i < nn; ++i)
+      for (int j = 0; j < nn; ++j) {
+        double s = 0.0;
+        for (int a = 0; a < nn; ++a)
+          for (int b = 0; b < nn; ++b) s += lch[a * nn + i] * ap[a * nn + b] * lch[b * nn + j];
+        sym[i * nn + j] = s;
+      }
+    jacobi(nn, sym, k2, v);
+    double *kl = kk + lc * nn;
+    double *g = gc + (size_t)lc * nstr * nstr;
+    /* X = W^-1 D^1/2 L V ; Y = (alpha+beta) X / k (DISORT SOLEIG form) */
+    double x[MAXNN * MAXNN], apb[MAXNN * MAXNN];
+    for (int i = 0; i < nn; ++i)
+      for (int j = 0; j < nn; ++j) {
+        double s = 0.0;
+        for (int a = 0; a <= i; ++a) s += lch[i * nn + a] * v[a * nn + j];
+        x[i * nn + j] = sd[i] / cwt[i] * s;
+        apb[i * nn + j] = (cc[i * nstr + j] + cc[i * nstr + nn + j] - (i == j)) / cmu[i];
+      }
+    for (int j = 0; j < nn; ++j) {
+      if (!(k2[j] > 0.0)) return 3;
+      kl[j] = sqrt(k2[j]);
+    }
+    for (int i = 0; i < nn; ++i)
+      for (int j = 0; j < nn; ++j) {
+        double y = 0.0;
+        for (int a = 0; a < nn; ++a) y += apb[i * nn + a] * x[a * nn + j];
+        y /= kl[j];
+        double gp = 0.5 * (x[i * nn + j] + y), gm = 0.5 * (x[i * nn + j] - y);
+        g[i * nstr + j] = gp;            /* up rows, +k mode */
+        g[(nn + i) * nstr + j] = gm;     /* down rows, +k mode */
+        g[i * nstr + nn + j] = gm;       /* up rows, -k mode */
+        g[(nn + i) * nstr + nn + j] = gp;
+      }
+    /* upbeam */
+    double a2[MAXN * MAXN];
+    int piv[MAXN];
+    if (beam) {
+      double *z = zb + lc * nstr;
+      for (int i = 0; i < nstr; ++i) {
+        double s = 0.0;
+        for (int l = 0; l < nstr; ++l) s += gl[l] * ylm[l][i] * p0[l];
+        z[i] = in->fbeam / (4.0 * PI) * s;
+        for (int j = 0; j < nstr; ++j)
+          a2[i * nstr + j] = (i == j ? 1.0 + cmuf[i] / in->umu0 : 0.0) - cc[i * nstr + j];
+      }
+      lu_factor(nstr, a2, piv);
+      lu_solve(nstr, a2, piv, z);
+    } else {
+      for (int i = 0; i < nstr; ++i) zb[lc * nstr + i] = 0.0;
+    }
+    /* upisot */
+    double *zz0 = z0 + lc * nstr, *zz1 = z1 + lc * nstr;
+    if (in->planck) {
+      double xr1 = dtaucp[lc] > 0.0 ? (pkag[lc + 1] - pkag[lc]) / dtaucp[lc] : 0.0;
+      double xr0 = pkag[lc] - xr1 * taucpr[lc];
+      for (int i = 0; i < nstr; ++i)
+        for (int j = 0; j < nstr; ++j) a2[i * nstr + j] = (i == j) - cc[i * nstr + j];
+      lu_factor(nstr, a2, piv);
+      for (int i = 0; i < nstr; ++i) zz1[i] = (1.0 - oprim[lc]) * xr1;
+      lu_solve(nstr, a2, piv, zz1);
+      for (int i = 0; i < nstr; ++i) zz0[i] = (1.0 - oprim[lc]) * xr0 + cmuf[i] * zz1[i];
+      lu_solve(nstr, a2, piv, zz0);
+    } else {
+      for (int i = 0; i < nstr; ++i) zz0[i] = zz1[i] = 0.0;
+    }
+  }
+
+#define ZP(lc, i, tau)                                                                   \
+  (z0[(lc) * nstr + (i)] + z1[(lc) * nstr + (i)] * (tau) +                             \
+   (beam ? zb[(lc) * nstr + (i)] * exp(-(tau) / in->umu0) : 0.0))
+#define GCT(lc, i, j) /* intensity at layer top: gc * [1, e] */                        \
+  (gc[(size_t)(lc) * nstr * nstr + (i) * nstr + (j)] *                                  \
+   ((j) < nn ? 1.0 : exp(-kk[(lc) * nn + (j) - nn] * dtaucp[lc])))
+#define GCB(lc, i, j) /* intensity at layer bottom: gc * [e, 1] */                     \
+  (gc[(size_t)(lc) * nstr * nstr + (i) * nstr + (j)] *                                  \
+   ((j) < nn ? exp(-kk[(lc) * nn + (j)] * dtaucp[lc]) : 1.0))
+#define AB(i, j) ab[(size_t)(j) * ld + kv + (i) - (j)]
+
+  /* ---- setmtx: banded BC matrix ---- */
+  const int kv = 2 * bw;
+  memset(ab, 0, sizeof(double) * (size_t)ld * ncol);
+  for (int i = 0; i < nn; ++i) { /* TOA: downward streams */
+    for (int j = 0; j < nstr; ++j) AB(i, j) = GCT(0, nn + i, j);
+    rhs[i] = in->fisot + tplanck - ZP(0, nn + i, 0.0);
+  }
+  for (int lc = 0; lc < nlyr - 1; ++lc) {
+    const double tau = taucpr[lc + 1];
+    for (int i = 0; i < nstr; ++i) {
+      const int r = nn + lc * nstr + i;
+      for (int j = 0; j < nstr; ++j) {
+        AB(r, lc * nstr + j) = GCB(lc, i, j);
+        AB(r, (lc + 1) * nstr + j) = -GCT(lc + 1, i, j);
+      }
+      rhs[r] = ZP(lc + 1, i, tau) - ZP(lc, i, tau);
+    }
+  }
+  {
+    const int lc = nlyr - 1;
+    const double tau = taucpr[nlyr];
+    double srf = (1.0 - in->albedo) * bplanck;
+    if (beam) srf += in->albedo * in->umu0 * in->fbeam * exp(-tau / in->umu0) / PI;
+    for (int i = 0; i < nn; ++i) {
+      const int r = nn + lc * nstr + i;
+      double zr = ZP(lc, i, tau);
+      for (int k = 0; k < nn; ++k) zr -= 2.0 * in->albedo * cwt[k] * cmu[k] * ZP(lc, nn + k, tau);
+      for (int j = 0; j < nstr; ++j) {
+        double a = GCB(lc, i, j);
+        for (int k = 0; k < nn; ++k) a -= 2.0 * in->albedo * cwt[k] * cmu[k] * GCB(lc, nn + k, j);
+        AB(r, lc * nstr + j) = a;
+      }
+      rhs[r] = srf - zr;
+    }
+  }
+  if (gb_factor(ncol, bw, bw, ab, ld, ipiv)) return 4;
+  gb_solve(ncol, bw, bw, ab, ld, ipiv, rhs);
+
+  /* ---- fluxes at the layer boundaries ---- */
+  for (int lev = 0; lev <= nlyr; ++lev) {
+    const int lc = lev == 0 ? 0 : lev - 1;
+    const double tau = taucpr[lev];
+    double up = 0.0, dn = 0.0;
+    for (int i = 0; i < nstr; ++i) {
+      double u = ZP(lc, i, tau);
+      for (int j = 0; j < nstr; ++j)
+        u += (lev == 0 ? GCT(0, i, j) : GCB(lc, i, j)) * rhs[lc * nstr + j];
+      if (i < nn) up += cwt[i] * cmu[i] * u;
+      else dn += cwt[i - nn] * cmu[i - nn] * u;
+    }
+    flup[lev] = 2.0 * PI * up;
+    double fdn = 2.0 * PI * dn, dir = 0.0;
+    if (beam) {
+      fdn += in->umu0 * in->fbeam * exp(-taucpr[lev] / in->umu0);
+      dir = in->umu0 * in->fbeam * exp(-tauc[lev] / in->umu0);
+    }
+    rfldir[lev] = dir;
+    rfldn[lev] = fdn - dir;
+  }
+#undef ZP
+#undef GCT
+#undef GCB
+#undef AB
+  return 0;
+}
+
+/* public: one column in cdisort conventions (for known-answer tests) */
+int hdo_column(int nstr, int nlyr, int nmom, const double *dtauc, const double *ssalb,
+               const double *pmom, int planck, const double *temper, double umu0,
+               double fbeam, double albedo, double fisot, double btemp, double ttemp,
+               double temis, double wvnmlo, double wvnmhi, double *rfldir, double *rfldn,
+               double *flup) {
+  hdo_column_in in = {nstr, nlyr, nmom, planck, dtauc, ssalb, pmom, temper,
+                      umu0, fbeam, albedo, fisot, btemp, ttemp, temis, wvnmlo, wvnmhi};
+  hdo_ws ws = {0, 0, 0, 0};
+  int rc = solve_column(&in, rfldir, rfldn, flup, &ws);
+  free(ws.work);
+  free(ws.iwork);
+  return rc;
+}
+
+/*
+ * public: harp-layout batch driver (pydisort DisortImpl::forward contract).
+ * prop [nwave][ncol][nlyr][nprop] (layer 0 = bottom); bc arrays [nwave][ncol]
+ * or NULL; temf [ncol][nlyr+1] bottom->top; flux [nwave][ncol][nlyr+1][2],
+ * level 0 = surface.  Solves s in [first, first+count) of the flattened
+ * (wave, col) index.  Returns the number of failed solves.
+ */
+long hdo_forward(int nwave, int ncol, int nlyr, int nprop, int nstr, int nmom, int planck,
+                 const double *prop, const double *fbeam, const double *umu0,
+                 const double *albedo, const double *btemp, const double *ttemp,
+                 const double *temis, const double *fisot, const double *temf,
+                 const double *wave_lower, const double *wave_upper, double *flux,
+                 int nthreads, long first, long count) {
+  long nsolve = (long)nwave * ncol;
+  if (first < 0) first = 0;
+  if (count < 0 || first + count > nsolve) count = nsolve - first;
+  int nm = nprop - 2 < nmom ? nprop - 2 : nmom;
+  if (nm < 0) nm = 0;
+  long nfail = 0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#else
+  (void)nthreads;
+#endif
+#pragma omp parallel reduction(+ : nfail)
+  {
+    hdo_ws ws = {0, 0, 0, 0};
+    double *dtauc = (double *)malloc(sizeof(double) * nlyr);
+    double *ssalb = (double *)malloc(sizeof(double) * nlyr);
+    double *pm = (double *)malloc(sizeof(double) * nlyr * (nm + 1));
+    double *tem = (double *)malloc(sizeof(double) * (nlyr + 1));
+    double *o1 = (double *)malloc(sizeof(double) * (nlyr + 1));
+    double *o2 = (double *)malloc(sizeof(double) * (nlyr + 1));
+    double *o3 = (double *)malloc(sizeof(double) * (nlyr + 1));
+#pragma omp for schedule(dynamic, 4)
+    for (long s = first; s < first + count; ++s) {
+      const int w = (int)(s / ncol), c = (int)(s % ncol);
+      const double *p = prop + (size_t)s * nlyr * nprop;
+      for (int lc = 0; lc < nlyr; ++lc) {
+        const double *q = p + (size_t)(nlyr - 1 - lc) * nprop;
+        dtauc[lc] = q[0];
+        ssalb[lc] = nprop > 1 ? q[1] : 0.0;
+        pm[lc * (nm + 1)] = 1.0;
+        for (int k = 1; k <= nm; ++k) pm[lc * (nm + 1) + k] = q[1 + k];
+      }
+      hdo_column_in in;
+      in.nstr = nstr; in.nlyr = nlyr; in.nmom = nm; in.planck = planck;
+      in.dtauc = dtauc; in.ssalb = ssalb; in.pmom = pm; in.temper = tem;
+      in.umu0 = umu0 ? umu0[s] : 1.0;
+      in.fbeam = fbeam ? fbeam[s] : 0.0;
+      in.albedo = albedo ? albedo[s] : 0.0;
+      in.fisot = fisot ? fisot[s] : 0.0;
+      in.btemp = btemp ? btemp[s] : 0.0;
+      in.ttemp = ttemp ? ttemp[s] : 0.0;
+      in.temis = temis ? temis[s] : 0.0;
+      in.wvnmlo = wave_lower ? wave_lower[w] : 0.0;
+      in.wvnmhi = wave_upper ? wave_upper[w] : 0.0;
+      if (planck)
+        for (int l = 0; l <= nlyr; ++l) tem[l] = temf[(size_t)c * (nlyr + 1) + nlyr - l];
+      double *fo = flux + (size_t)s * (nlyr + 1) * 2;
+      if (solve_column(&in, o1, o2, o3, &ws)) {
+        nfail++;
+        for (int l = 0; l <= nlyr; ++l) fo[2 * l] = fo[2 * l + 1] = NAN;
+        continue;
+      }
+      for (int l = 0; l <= nlyr; ++l) {
+        fo[2 * l] = o3[nlyr - l];
+        fo[2 * l + 1] = o1[nlyr - l] + o2[nlyr - l];
+      }
+    }
+    free(ws.work); free(ws.iwork);
+    free(dtauc); free(ssalb); free(pm); free(tem); free(o1); free(o2); free(o3);
+  }
+  return nfail;
+}
