@@ -1,0 +1,276 @@
+"""Benchmark of the DISORT flux hot path on MI355X (driver contract).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--planck] [--ncol C]
+
+Workload (BASELINE.json configs[3], SURVEY.md 8(d) "C4 GCM"): 1e4 synthetic
+columns x 64 g-points, nstr=16, nmom=16 (Henyey-Greenstein chi_l = g^l),
+nlyr=80, tau log-uniform [1e-5, 5], omega in [0, 0.99], g in [0, 0.85],
+umu0 in [0.05, 1], albedo in [0, 1], fbeam = 1 (``--planck`` adds thermal
+emission, T 150-300 K).  One step = one flux solve of every (g-point, column)
+pair of the rank's shard (hd_solve through the C-ABI) + the g-weighted band
+flux (C, L+1, 2), all-reduced over ranks.  Inputs are generated on the device
+before the timed region (seeded per g-point, so the global problem does not
+depend on N).  Spectral sharding: rank r owns g-points {g : g mod N == r}
+(fixed global problem -> "scaling": "strong").
+
+Printed (rank 0): one JSON line with the contract fields plus
+  roofline      dominant kernel (hd_layer_kernel), algorithmic FLOP per launch
+                / average launch time from HIP events on the solve stream
+  cpu_baseline  oracle/ C restatement (a port of the DISORT algorithm, not
+                cdisort, which is absent) timed on the host cores, N=1 only
+  max_rel_err   GPU vs that CPU restatement on a subsample of the workload
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "DISORT column-solves/sec (nstr=16, nlyr=80); max |dF|/F vs cdisort"
+FP64_PEAK_TFLOPS = 78.6  # MI355X: 256 CU x 2.4 GHz x 128 FP64 FLOP/clk (vector = matrix)
+HBM_PEAK_GBS = 8000.0
+
+
+def algorithmic_flop(nstr: int, nlyr: int, planck: bool):
+    """SURVEY.md 8(d) convention: per solve L*(10.5 n^3 + 12 n^2) (+ L*(2/3 n^3 + 4 n^2) planck).
+
+    Split per kernel: per-layer setup (assembly 1.5n^3 + eigen 3.625n^3 + beam
+    LU 2/3 n^3, + Planck LU) -> hd_layer_kernel; boundary sweep (14/3 n^3 +
+    12 n^2) -> hd_sweep_kernel.
+    """
+    n = float(nstr)
+    k1 = nlyr * (1.5 + 3.625 + 2.0 / 3.0) * n ** 3
+    k2 = nlyr * (14.0 / 3.0 * n ** 3 + 12.0 * n ** 2)
+    total = nlyr * (10.5 * n ** 3 + 12.0 * n ** 2)
+    if planck:
+        k1 += nlyr * (2.0 / 3.0 * n ** 3 + 4.0 * n ** 2)
+        total += nlyr * (2.0 / 3.0 * n ** 3 + 4.0 * n ** 2)
+    return total, k1, k2
+
+
+def make_inputs(gpoints, ncol, nlyr, nstr, planck, dev, seed=20250217):
+    """Synthetic C4 inputs for the given g-points, generated on `dev`."""
+    nmom = nstr
+    W = len(gpoints)
+    f64 = torch.float64
+    prop = torch.empty((W, ncol, nlyr, 2 + nmom), dtype=f64, device=dev)
+    bc = {k: torch.empty((W, ncol), dtype=f64, device=dev) for k in ("fbeam", "umu0", "albedo")}
+    if planck:
+        bc["btemp"] = torch.empty((W, ncol), dtype=f64, device=dev)
+    for i, g in enumerate(gpoints):
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(seed * 1000 + int(g))
+        r = lambda *shape: torch.rand(shape, generator=gen, dtype=f64, device=dev)  # noqa: E731
+        prop[i, ..., 0] = 10.0 ** (r(ncol, nlyr) * np.log10(5.0 / 1e-5) - 5.0)
+        prop[i, ..., 1] = 0.99 * r(ncol, nlyr)
+        gg = 0.85 * r(ncol, nlyr)
+        for l in range(nmom):
+            prop[i, ..., 2 + l] = gg ** (l + 1)
+        bc["fbeam"][i] = 1.0
+        bc["umu0"][i] = 0.05 + 0.95 * r(ncol)
+        bc["albedo"][i] = r(ncol)
+        if planck:
+            bc["btemp"][i] = 300.0
+    temf = None
+    if planck:
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(seed)
+        tl = torch.linspace(300.0, 150.0, nlyr, dtype=f64, device=dev)[None, :] + \
+            5.0 * (torch.rand((ncol, nlyr), generator=gen, dtype=f64, device=dev) - 0.5)
+        from pyharp_amd import layer2level
+        temf = layer2level(tl)
+    return prop, bc, temf
+
+
+def gpoint_weights(ngpoint):
+    # fixed synthetic correlated-k weights (sum to 1)
+    x = np.arange(ngpoint, dtype=np.float64)
+    w = 1.0 + 0.5 * np.cos(x)
+    return w / w.sum()
+
+
+def wave_bounds(ngpoint):
+    lo = 10.0 + 30.0 * np.arange(ngpoint, dtype=np.float64)
+    return lo, lo + 30.0
+
+
+def load_pmc(workload: str):
+    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        if d.get("workload") != workload:
+            return None
+        return d
+    except Exception:
+        return None
+
+
+def cpu_baseline(prop, bc, temf, nstr, planck, wl, wu, target_s=12.0):
+    """Time the C restatement (oracle/) on a bounded sample of the same workload."""
+    from oracle import oracle_c
+    oracle_c.build()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    # up to 4 g-point slabs of the same workload on the host
+    m = min(prop.shape[0], 4)
+    p = prop[:m].cpu().numpy()
+    b = {k: v[:m].cpu().numpy() for k, v in bc.items()}
+    tf = None if temf is None else temf.cpu().numpy()
+    kw = dict(nstr=nstr, planck=planck, wave_lower=wl[:m], wave_upper=wu[:m], nthreads=threads)
+    out = np.zeros((m, p.shape[1], p.shape[2] + 1, 2))
+    n_cal = min(m * p.shape[1], 8 * threads)
+    t0 = time.perf_counter()
+    oracle_c.forward(p, b, tf, first=0, count=n_cal, out=out, **kw)
+    dt = time.perf_counter() - t0
+    n = int(min(m * p.shape[1], max(n_cal, n_cal * target_s / max(dt, 1e-6))))
+    t0 = time.perf_counter()
+    oracle_c.forward(p, b, tf, first=0, count=n, out=out, **kw)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "column-solves/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} (g-point, column) solves of the same workload (nstr={nstr}, "
+                      f"nlyr={p.shape[2]}), {threads} OpenMP threads, {dt:.1f} s; "
+                      "oracle/disort_oracle.c = C restatement of the DISORT algorithm "
+                      "(cdisort itself is absent from the reference)"}, out, n
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--ncol", type=int, default=10000)
+    ap.add_argument("--ngpoint", type=int, default=64)
+    ap.add_argument("--nlyr", type=int, default=80)
+    ap.add_argument("--nstr", type=int, default=16)
+    ap.add_argument("--planck", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    from pyharp_amd import Disort, DisortOptions
+    from pyharp_amd.disort import _context
+
+    ncol, nlyr, nstr, G = args.ncol, args.nlyr, args.nstr, args.ngpoint
+    gpoints = [g for g in range(G) if g % world == rank]
+    W = len(gpoints)
+    wl_all, wu_all = wave_bounds(G)
+    wl, wu = wl_all[gpoints], wu_all[gpoints]
+    prop, bc, temf = make_inputs(gpoints, ncol, nlyr, nstr, args.planck, dev)
+    wts = torch.tensor(gpoint_weights(G)[gpoints], dtype=torch.float64, device=dev)
+
+    op = DisortOptions().flags("lamber,quiet,onlyfl" + (",planck" if args.planck else ""))
+    op.nwave(W).ncol(ncol).device(local_rank)
+    if args.planck:
+        op.wave_lower(list(wl)).wave_upper(list(wu))
+    op.ds().nlyr, op.ds().nstr, op.ds().nmom = nlyr, nstr, nstr
+    disort = Disort(op)
+    flux = torch.empty((W, ncol, nlyr + 1, 2), dtype=torch.float64, device=dev)
+    status = torch.zeros(W * ncol, dtype=torch.int32, device=dev)
+
+    def step():
+        disort.forward(prop, bc, temf, status=status, out=flux)
+        band = torch.einsum("g,gcld->cld", wts, flux)
+        if world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(band)
+        return band
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if int((status & 0xF).any()):
+        raise RuntimeError("bench: solver reported errors in the warm-up")
+    ctx = _context(local_rank)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    ctx.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        band = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    tm = ctx.timing()
+    ctx.set_timing(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    nsolve_total = G * ncol
+    value = nsolve_total * args.steps / elapsed
+    total_flop, k1_flop, k2_flop = algorithmic_flop(nstr, nlyr, args.planck)
+    workload = (f"C4 GCM batch: {ncol} columns x {G} g-points, nstr={nstr}, nmom={nstr}, "
+                f"nlyr={nlyr}, beam{' + planck' if args.planck else ''}")
+
+    if rank == 0:
+        # dominant kernel roofline (hd_layer_kernel), per launch
+        k1_avg_ms = tm.layer_ms / max(tm.layer_launches, 1)
+        solves_per_launch = W * ncol * args.steps / max(tm.layer_launches, 1)
+        ach = k1_flop * solves_per_launch / (k1_avg_ms * 1e-3) / 1e12
+        pmc = load_pmc(workload)
+        roofline = {"bound": "mfma", "kernel": "hd_layer_kernel", "achieved": round(ach, 3),
+                    "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(ach / FP64_PEAK_TFLOPS, 4),
+                    "traffic": (pmc or {}).get("layer_kernel_bytes_per_launch"),
+                    "avg_launch_ms": round(k1_avg_ms, 3),
+                    "flop_per_solve": k1_flop,
+                    "note": "FP64 compute bound (gfx950 FP64 vector and MFMA peaks are equal); "
+                            "achieved uses the SURVEY 8(d) algorithmic FLOP convention"}
+        whole = {"achieved_tflops": round(total_flop * value / 1e12, 3),
+                 "frac": round(total_flop * value / 1e12 / FP64_PEAK_TFLOPS / world, 4),
+                 "layer_ms_per_step": round(tm.layer_ms / args.steps, 3),
+                 "sweep_ms_per_step": round(tm.sweep_ms / args.steps, 3)}
+        cpu = None
+        max_err = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu, ref, n = cpu_baseline(prop, bc, temf, nstr, args.planck, wl, wu)
+            m = ref.shape[0]
+            got = flux[:m].cpu().numpy().reshape(-1, nlyr + 1, 2)[:n]
+            r = ref.reshape(-1, nlyr + 1, 2)[:n]
+            scale = np.abs(r).max(axis=(1, 2), keepdims=True)
+            max_err = float((np.abs(got - r) / np.maximum(np.abs(r), 1e-6 * scale)).max())
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "column-solves/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": workload, "ncol": ncol, "ngpoint": G, "nstr": nstr,
+                       "nmom": nstr, "nlyr": nlyr, "planck": bool(args.planck),
+                       "parallelism": f"spectral g mod {world}",
+                       "collective": "all_reduce of the g-weighted band flux (RCCL)" if world > 1
+                       else "none"},
+            "roofline": roofline, "path_roofline": whole, "cpu_baseline": cpu,
+            "max_rel_err_vs_cpu_restatement": max_err,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,121 @@
+/*
+ * hdisort.h -- C-ABI of the MI355X-native flux-only discrete-ordinate
+ * radiative-transfer solver (libhdisort.so, HIP kernels for gfx950).
+ *
+ * This is the drop-in boundary for pyharp's RT-solver plugin path.  It
+ * replaces, for the flux-only case (onlyfl, lamber, azimuthal mode m=0):
+ *
+ *   - pydisort's batch driver  disort::DisortImpl::forward(prop, &bc[, temf])
+ *       [EXTERNAL, pydisort @ afee3ec897f, cmake/pydisort.cmake:9-11]
+ *     called at examples/amars_sw.cpp:280, examples/amars_lw.cpp:80,
+ *     tests/test_disort.cpp:49, src/radiation/radiation_band.cpp:124-127,
+ *     behind the plugin signature RTSolverImpl::forward(prop, bc, temf)
+ *     (src/rtsolver/rtsolver.hpp:25-29);
+ *   - the per-column cdisort call  c_disort(&ds_, &ds_out_)
+ *     (legacy site src/rtsolver/rt_solver_disort.cpp_:147,234).
+ *
+ * Layouts follow the harp call sites:
+ *   prop  [nwave][ncol][nlyr][nprop] f64, layer 0 = bottom
+ *         slot 0 = layer optical thickness, 1 = single-scattering albedo,
+ *         2.. = phase moments chi_1..chi_nmom (chi_0 = 1 implicit)
+ *         (src/index.h:12-18, src/radiation/radiation_band.cpp:116)
+ *   bc    per-solve arrays [nwave][ncol] f64 (NULL = default): fbeam (0),
+ *         umu0 (1), albedo (0), btemp (0), ttemp (0), temis (0), fisot (0)
+ *         (src/radiation/radiation_band.hpp:74-77, amars_sw.cpp:276-278,
+ *          amars_lw.cpp:73-74)
+ *   temf  [ncol][nlyr+1] f64 level temperatures, level 0 = bottom (planck)
+ *         (amars_lw.cpp:76, src/utils/layer2level.hpp:41)
+ *   wave_lower/upper [nwave] f64 wavenumber bounds [cm^-1] (planck)
+ *   flux  [nwave][ncol][nlyr+1][2] f64, level 0 = surface,
+ *         [..][0] = upward flux, [..][1] = rfldir + rfldn
+ *         (src/rtsolver/rt_solver_disort.cpp_:172-181, amars_sw.cpp:185-191)
+ * All array pointers are DEVICE pointers (hipMalloc / torch cuda tensors).
+ *
+ * Errors never cross the ABI as exceptions: every entry point returns an
+ * hd_status code; hd_last_error() gives the message.
+ */
+#ifndef HDISORT_H_
+#define HDISORT_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HDISORT_VERSION 100 /* 1.0.0 */
+
+/* return codes */
+#define HD_OK 0
+#define HD_EINVAL 1    /* bad argument / shape / flag                         */
+#define HD_ENUMERIC 2  /* at least one solve set an error bit (see status)    */
+#define HD_EHIP 3      /* HIP runtime error                                   */
+#define HD_ENOMEM 4    /* device allocation failed                            */
+
+/* hd_config.flags (subset of the pydisort flag string that this path keeps) */
+#define HD_FLAG_LAMBER 0x1u /* Lambertian lower boundary (always on)          */
+#define HD_FLAG_PLANCK 0x2u /* thermal emission (needs temf, wave bounds)     */
+#define HD_FLAG_ONLYFL 0x4u /* fluxes only (always on: the only mode here)    */
+
+/* per-solve status bits (int32 per solve) */
+#define HD_STATUS_BAD_INPUT 0x01 /* tau<0, ssa outside [0,1], f>=1, umu0>1 ... */
+#define HD_STATUS_EIGEN 0x02     /* eigenvalue <= 0 / Cholesky breakdown         */
+#define HD_STATUS_NONFINITE 0x04 /* NaN/Inf produced                             */
+#define HD_STATUS_RESONANCE 0x10 /* warning: umu0 ~ 1/k (beam/quadrature resonance) */
+#define HD_STATUS_PIVOT 0x20     /* warning: tiny pivot in the boundary sweep      */
+#define HD_STATUS_ERROR_MASK 0x0F
+
+typedef struct hd_config {
+  int nstr;       /* number of streams, even, 2..16 */
+  int nmom;       /* phase moments the module was configured with (>= 0)   */
+  int nlyr;       /* layers                                                 */
+  int nprop;      /* last-dim size of prop (>= 1); moments used = min(nmom, nprop-2) */
+  unsigned flags; /* HD_FLAG_*                                              */
+} hd_config;
+
+typedef struct hd_inputs {
+  int nwave, ncol;
+  const double *prop;
+  const double *fbeam, *umu0, *albedo, *btemp, *ttemp, *temis, *fisot;
+  const double *temf;
+  const double *wave_lower, *wave_upper;
+} hd_inputs;
+
+/* per-kernel device time accumulated since hd_context_set_timing(ctx, 1): HIP events
+ * recorded on the solve stream around every launch, resolved lazily by get_timing */
+typedef struct hd_timing {
+  double layer_ms;  /* sum over launches of hd_layer_kernel (per-layer setup)  */
+  double sweep_ms;  /* sum over launches of hd_sweep_kernel (boundary sweep)   */
+  int layer_launches;
+  int sweep_launches;
+} hd_timing;
+
+typedef struct hd_context hd_context;
+
+int hd_version(void);
+const char *hd_last_error(const hd_context *ctx); /* ctx may be NULL (global) */
+
+int hd_context_create(hd_context **ctx, int device);
+int hd_context_destroy(hd_context *ctx);
+/* max solves per internal chunk (scratch = chunk*nlyr*~1.4 KB); 0 = auto */
+int hd_context_set_chunk(hd_context *ctx, long max_solves);
+int hd_context_set_timing(hd_context *ctx, int enable);
+int hd_context_get_timing(const hd_context *ctx, hd_timing *out);
+/* pre-size scratch for graph capture / steady state */
+int hd_context_reserve(hd_context *ctx, const hd_config *cfg, long nsolve);
+
+/*
+ * Solve every (wave, column) flux problem of the batch on `stream`
+ * (hipStream_t passed as void*; NULL = default stream).
+ * status: device int32[nwave*ncol] or NULL.  With NULL the call is
+ * synchronous and returns HD_ENUMERIC if any solve set an error bit; with a
+ * caller buffer the call is asynchronous and the caller inspects it.
+ */
+int hd_solve(hd_context *ctx, const hd_config *cfg, const hd_inputs *in, double *flux,
+             int *status, void *stream);
+
+/* host helper: the double-Gauss quadrature the kernels use (nstr/2 nodes on (0,1)) */
+int hd_quadrature(int nstr, double *mu, double *w);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HDISORT_H_ */

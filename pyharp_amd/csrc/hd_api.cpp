@@ -1,0 +1,400 @@
+// hd_api.cpp -- C-ABI of libhdisort.so (include/hdisort.h): argument
+// validation, quadrature constants, scratch management, chunked launches,
+// per-solve status, optional per-kernel timing with HIP events.
+//
+// Replaces pydisort's DisortImpl::forward batch loop over (nwave, ncol)
+// [EXTERNAL, pydisort @ afee3ec897f] and its per-column c_disort calls
+// (legacy: src/rtsolver/rt_solver_disort.cpp_:147,234; error behaviour:
+// nonzero c_disort -> "DisortWrapper::Run failed.", :149-151).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/hdisort.h"
+#include "hd_kernels.hpp"
+
+struct hd_context {
+  int device = 0;
+  double* scratch = nullptr;
+  size_t scratch_doubles = 0;
+  int* status = nullptr;  // internal per-solve status (when caller passes NULL)
+  size_t status_len = 0;
+  int* anyerr = nullptr;
+  long chunk = 0;  // 0 = auto
+  bool timing = false;
+  // timing: one event triple per launched chunk, resolved lazily in get_timing
+  std::vector<hipEvent_t> pool;
+  size_t pool_used = 0;
+  bool tables = false;
+  hd_timing times{};
+  std::string err;
+};
+
+namespace {
+
+std::mutex g_err_mu;
+std::string g_err;
+
+int fail(hd_context* ctx, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (ctx) ctx->err = buf;
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  g_err = buf;
+  return code;
+}
+
+#define HD_HIP(ctx, call)                                                                   \
+  do {                                                                                      \
+    hipError_t e_ = (call);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      return fail(ctx, HD_EHIP, "%s failed: %s", #call, hipGetErrorString(e_));            \
+  } while (0)
+
+// Gauss-Legendre nodes/weights on (0,1), ascending (double-Gauss half range).
+void gauss01(int nn, double* mu, double* w) {
+  const double pi = 3.14159265358979323846;
+  for (int i = 0; i < (nn + 1) / 2; ++i) {
+    double x = std::cos(pi * (i + 0.75) / (nn + 0.5));
+    double dp = 1.0;
+    for (int it = 0; it < 100; ++it) {
+      double p0 = 1.0, p1 = x;
+      for (int l = 2; l <= nn; ++l) {
+        double p2 = ((2 * l - 1) * x * p1 - (l - 1) * p0) / l;
+        p0 = p1;
+        p1 = p2;
+      }
+      dp = nn * (x * p1 - p0) / (x * x - 1.0);
+      double dx = p1 / dp;
+      x -= dx;
+      if (std::fabs(dx) < 1e-16) break;
+    }
+    {
+      double p0 = 1.0, p1 = x;
+      for (int l = 2; l <= nn; ++l) {
+        double p2 = ((2 * l - 1) * x * p1 - (l - 1) * p0) / l;
+        p0 = p1;
+        p1 = p2;
+      }
+      dp = nn * (x * p1 - p0) / (x * x - 1.0);
+    }
+    const double wx = 2.0 / ((1.0 - x * x) * dp * dp);
+    mu[nn - 1 - i] = 0.5 * (1.0 + x);
+    w[nn - 1 - i] = 0.5 * wx;
+    mu[i] = 0.5 * (1.0 - x);
+    w[i] = 0.5 * wx;
+  }
+}
+
+void make_quad(int nn, hd::QuadHost& q) {
+  std::memset(&q, 0, sizeof(q));
+  gauss01(nn, q.mu, q.w);
+  for (int i = 0; i < nn; ++i) {
+    q.sd[i] = std::sqrt(q.w[i] / q.mu[i]);
+    q.g[i] = std::sqrt(q.w[i] * q.mu[i]);
+    double p0 = 1.0, p1 = q.mu[i];
+    q.pt[0][i] = 1.0;
+    if (2 * nn > 1) q.pt[1][i] = p1;
+    for (int l = 2; l < 2 * nn; ++l) {
+      double p2 = ((2 * l - 1) * q.mu[i] * p1 - (l - 1) * p0) / l;
+      q.pt[l][i] = p2;
+      p0 = p1;
+      p1 = p2;
+    }
+  }
+}
+
+int ensure_tables(hd_context* ctx) {
+  if (ctx->tables) return HD_OK;
+  static hd::QuadHost all[hd::kMaxNN];
+  for (int nn = 1; nn <= hd::kMaxNN; ++nn) make_quad(nn, all[nn - 1]);
+  hipError_t e = hd::upload_quad_tables(all);
+  if (e != hipSuccess) return fail(ctx, HD_EHIP, "hd_solve: constant upload: %s", hipGetErrorString(e));
+  ctx->tables = true;
+  return HD_OK;
+}
+
+long auto_chunk(long nsolve, int nlyr) {
+  // Enough solves per chunk to fill 256 CUs with the one-lane-per-solve sweep,
+  // bounded so the scratch stays well inside HBM.
+  const long cap = std::max<long>(65536, (long)(4096L * 1024L * 1024L / 8 / 200) / std::max(1, nlyr));
+  long target = std::min<long>(cap, 262144);
+  if (nsolve <= target) return nsolve;
+  long n = (nsolve + target - 1) / target;
+  return (nsolve + n - 1) / n;
+}
+
+int ensure_scratch(hd_context* ctx, size_t ndoubles) {
+  if (ctx->scratch_doubles >= ndoubles) return HD_OK;
+  if (ctx->scratch) (void)hipFree(ctx->scratch);
+  ctx->scratch = nullptr;
+  ctx->scratch_doubles = 0;
+  if (hipMalloc(&ctx->scratch, ndoubles * sizeof(double)) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(ctx, HD_ENOMEM, "hd_solve: cannot allocate %zu bytes of scratch",
+                ndoubles * sizeof(double));
+  }
+  ctx->scratch_doubles = ndoubles;
+  return HD_OK;
+}
+
+int ensure_status(hd_context* ctx, size_t n) {
+  if (ctx->status_len >= n) return HD_OK;
+  if (ctx->status) (void)hipFree(ctx->status);
+  ctx->status = nullptr;
+  ctx->status_len = 0;
+  if (hipMalloc(&ctx->status, std::max<size_t>(n, 1) * sizeof(int)) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(ctx, HD_ENOMEM, "hd_solve: cannot allocate status buffer");
+  }
+  ctx->status_len = n;
+  return HD_OK;
+}
+
+// fold every recorded (K1 start, K1 end = K2 start, K2 end) triple into the totals
+int resolve_timing(hd_context* ctx) {
+  for (size_t i = 0; i + 3 <= ctx->pool_used; i += 3) {
+    HD_HIP(ctx, hipEventSynchronize(ctx->pool[i + 2]));
+    float t1 = 0.f, t2 = 0.f;
+    HD_HIP(ctx, hipEventElapsedTime(&t1, ctx->pool[i], ctx->pool[i + 1]));
+    HD_HIP(ctx, hipEventElapsedTime(&t2, ctx->pool[i + 1], ctx->pool[i + 2]));
+    ctx->times.layer_ms += t1;
+    ctx->times.sweep_ms += t2;
+    ctx->times.layer_launches += 1;
+    ctx->times.sweep_launches += 1;
+  }
+  ctx->pool_used = 0;
+  return HD_OK;
+}
+
+int validate(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, const double* flux) {
+  if (!cfg || !in) return fail(ctx, HD_EINVAL, "hd_solve: null config/inputs");
+  if (cfg->nstr < 2 || cfg->nstr % 2 || cfg->nstr / 2 > hd::kMaxNN)
+    return fail(ctx, HD_EINVAL, "hd_solve: nstr=%d must be even and in [2, %d]", cfg->nstr,
+                2 * hd::kMaxNN);
+  if (cfg->nlyr < 1) return fail(ctx, HD_EINVAL, "hd_solve: nlyr=%d < 1", cfg->nlyr);
+  if (cfg->nprop < 1) return fail(ctx, HD_EINVAL, "hd_solve: nprop=%d < 1", cfg->nprop);
+  if (cfg->nmom < 0) return fail(ctx, HD_EINVAL, "hd_solve: nmom=%d < 0", cfg->nmom);
+  if (cfg->flags & ~(HD_FLAG_LAMBER | HD_FLAG_PLANCK | HD_FLAG_ONLYFL))
+    return fail(ctx, HD_EINVAL, "hd_solve: unsupported flags 0x%x", cfg->flags);
+  if (in->nwave < 0 || in->ncol < 0)
+    return fail(ctx, HD_EINVAL, "hd_solve: negative nwave/ncol");
+  if ((long)in->nwave * in->ncol > 0 && (!in->prop || !flux))
+    return fail(ctx, HD_EINVAL, "hd_solve: prop and flux are required");
+  if ((cfg->flags & HD_FLAG_PLANCK) && (!in->temf || !in->wave_lower || !in->wave_upper))
+    return fail(ctx, HD_EINVAL, "hd_solve: planck needs temf, wave_lower, wave_upper");
+  if ((long)in->nwave * in->ncol > (long)0x7fffffff)
+    return fail(ctx, HD_EINVAL, "hd_solve: nwave*ncol exceeds 2^31");
+  return HD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hd_version(void) { return HDISORT_VERSION; }
+
+const char* hd_last_error(const hd_context* ctx) {
+  if (ctx) return ctx->err.c_str();
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  static thread_local std::string copy;
+  copy = g_err;
+  return copy.c_str();
+}
+
+int hd_context_create(hd_context** out, int device) {
+  if (!out) return fail(nullptr, HD_EINVAL, "hd_context_create: null out");
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    (void)hipGetLastError();
+    return fail(nullptr, HD_EHIP, "hd_context_create: no HIP device available");
+  }
+  if (device < 0 || device >= ndev)
+    return fail(nullptr, HD_EINVAL, "hd_context_create: device %d out of range (%d)", device,
+                ndev);
+  hd_context* ctx = new hd_context();
+  ctx->device = device;
+  HD_HIP(ctx, hipSetDevice(device));
+  HD_HIP(ctx, hipMalloc(&ctx->anyerr, sizeof(int)));
+  *out = ctx;
+  return HD_OK;
+}
+
+int hd_context_destroy(hd_context* ctx) {
+  if (!ctx) return HD_OK;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->status) (void)hipFree(ctx->status);
+  if (ctx->anyerr) (void)hipFree(ctx->anyerr);
+  for (auto& e : ctx->pool)
+    if (e) (void)hipEventDestroy(e);
+  delete ctx;
+  return HD_OK;
+}
+
+int hd_context_set_chunk(hd_context* ctx, long max_solves) {
+  if (!ctx || max_solves < 0) return fail(ctx, HD_EINVAL, "hd_context_set_chunk: bad args");
+  ctx->chunk = max_solves;
+  return HD_OK;
+}
+
+int hd_context_set_timing(hd_context* ctx, int enable) {
+  if (!ctx) return fail(nullptr, HD_EINVAL, "hd_context_set_timing: null ctx");
+  ctx->timing = enable != 0;
+  ctx->pool_used = 0;  // (re)start accumulating
+  ctx->times = hd_timing{};
+  return HD_OK;
+}
+
+int hd_context_get_timing(const hd_context* ctx_, hd_timing* out) {
+  if (!ctx_ || !out) return fail(nullptr, HD_EINVAL, "hd_context_get_timing: null arg");
+  hd_context* ctx = const_cast<hd_context*>(ctx_);
+  int rc = resolve_timing(ctx);
+  if (rc) return rc;
+  *out = ctx->times;
+  return HD_OK;
+}
+
+int hd_context_reserve(hd_context* ctx, const hd_config* cfg, long nsolve) {
+  if (!ctx || !cfg || nsolve < 0) return fail(ctx, HD_EINVAL, "hd_context_reserve: bad args");
+  if (cfg->nstr < 2 || cfg->nstr % 2 || cfg->nstr / 2 > hd::kMaxNN || cfg->nlyr < 1)
+    return fail(ctx, HD_EINVAL, "hd_context_reserve: bad config");
+  HD_HIP(ctx, hipSetDevice(ctx->device));
+  const long chunk = ctx->chunk > 0 ? std::min(ctx->chunk, nsolve) : auto_chunk(nsolve, cfg->nlyr);
+  const size_t per = hd::scratch_doubles_per_solve(cfg->nstr / 2, cfg->nlyr,
+                                                   (cfg->flags & HD_FLAG_PLANCK) != 0);
+  int rc = ensure_scratch(ctx, per * std::max<long>(chunk, 1));
+  if (rc) return rc;
+  rc = ensure_tables(ctx);
+  if (rc) return rc;
+  return ensure_status(ctx, (size_t)nsolve);
+}
+
+int hd_quadrature(int nstr, double* mu, double* w) {
+  if (nstr < 2 || nstr % 2 || !mu || !w)
+    return fail(nullptr, HD_EINVAL, "hd_quadrature: bad args");
+  gauss01(nstr / 2, mu, w);
+  return HD_OK;
+}
+
+int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double* flux,
+             int* status, void* stream_) {
+  if (!ctx) return fail(nullptr, HD_EINVAL, "hd_solve: null context");
+  int rc = validate(ctx, cfg, in, flux);
+  if (rc) return rc;
+  const long nsolve = (long)in->nwave * in->ncol;
+  if (nsolve == 0) return HD_OK;
+  HD_HIP(ctx, hipSetDevice(ctx->device));
+  hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+  const int nn = cfg->nstr / 2;
+  const int nlyr = cfg->nlyr;
+  const bool planck = (cfg->flags & HD_FLAG_PLANCK) != 0;
+  const bool sync = status == nullptr;
+
+  long chunk = ctx->chunk > 0 ? std::min(ctx->chunk, nsolve) : auto_chunk(nsolve, nlyr);
+  const size_t ne1 = (size_t)(nn * (nn + 1) + 2 * nn + 1);
+  const size_t ne2 = (size_t)(nn * nn + 2 * nn + 1);
+  const size_t per = hd::scratch_doubles_per_solve(nn, nlyr, planck);
+  rc = ensure_scratch(ctx, per * chunk);
+  if (rc) return rc;
+  rc = ensure_tables(ctx);
+  if (rc) return rc;
+  if (sync) {
+    rc = ensure_status(ctx, (size_t)nsolve);
+    if (rc) return rc;
+    status = ctx->status;
+  }
+  HD_HIP(ctx, hipMemsetAsync(status, 0, sizeof(int) * nsolve, stream));
+  HD_HIP(ctx, hipMemsetAsync(ctx->anyerr, 0, sizeof(int), stream));
+  const int nm = std::max(0, std::min(cfg->nmom, cfg->nprop - 2));
+
+  for (long s0 = 0; s0 < nsolve; s0 += chunk) {
+    const int nsc = (int)std::min(chunk, nsolve - s0);
+    double* layer_ops = ctx->scratch;
+    double* bsub = layer_ops + ne1 * nlyr * (size_t)nsc;
+    double* planckv = planck ? bsub + ne2 * nlyr * (size_t)nsc : nullptr;
+    hd::PlanckArgs pa{};
+    pa.temf = in->temf;
+    pa.btemp = in->btemp;
+    pa.ttemp = in->ttemp;
+    pa.temis = in->temis;
+    pa.wlo = in->wave_lower;
+    pa.whi = in->wave_upper;
+    pa.out = planckv;
+    pa.s0 = s0;
+    pa.nsc = nsc;
+    pa.ncol = in->ncol;
+    pa.nlyr = nlyr;
+    hd::LayerArgs la{};
+    la.prop = in->prop;
+    la.fbeam = in->fbeam;
+    la.umu0 = in->umu0;
+    la.planckv = planckv;
+    la.scr = layer_ops;
+    la.status = status;
+    la.anyerr = ctx->anyerr;
+    la.s0 = s0;
+    la.nsc = nsc;
+    la.ncol = in->ncol;
+    la.nlyr = nlyr;
+    la.nprop = cfg->nprop;
+    la.nmom = nm;
+    la.planck = planck;
+    la.max_sweeps = 16;
+    hd::SweepArgs sa{};
+    sa.scr = layer_ops;
+    sa.bsub = bsub;
+    sa.flux = flux;
+    sa.fbeam = in->fbeam;
+    sa.umu0 = in->umu0;
+    sa.albedo = in->albedo;
+    sa.fisot = in->fisot;
+    sa.planckv = planckv;
+    sa.status = status;
+    sa.anyerr = ctx->anyerr;
+    sa.s0 = s0;
+    sa.nsc = nsc;
+    sa.ncol = in->ncol;
+    sa.nlyr = nlyr;
+    sa.planck = planck;
+    hipEvent_t* ev = nullptr;
+    if (ctx->timing) {
+      if (ctx->pool_used >= 3 * 512) {
+        rc = resolve_timing(ctx);
+        if (rc) return rc;
+      }
+      while (ctx->pool.size() < ctx->pool_used + 3) {
+        hipEvent_t e;
+        HD_HIP(ctx, hipEventCreate(&e));
+        ctx->pool.push_back(e);
+      }
+      ev = &ctx->pool[ctx->pool_used];
+      ctx->pool_used += 3;
+    }
+    hipError_t e = hd::launch_solve_chunk_nn(nn, planck ? &pa : nullptr, la, sa, stream, ev);
+    if (e != hipSuccess) return fail(ctx, HD_EHIP, "hd_solve: launch failed: %s", hipGetErrorString(e));
+  }
+  if (sync) {
+    int any = 0;
+    HD_HIP(ctx, hipMemcpyAsync(&any, ctx->anyerr, sizeof(int), hipMemcpyDeviceToHost, stream));
+    HD_HIP(ctx, hipStreamSynchronize(stream));
+    if (any)
+      return fail(ctx, HD_ENUMERIC,
+                  "hd_solve: at least one solve failed (bad input, eigen breakdown or non-finite "
+                  "result); DisortWrapper::Run failed.");
+  }
+  return HD_OK;
+}
+
+}  // extern "C"

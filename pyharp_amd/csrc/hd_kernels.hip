@@ -1,0 +1,788 @@
+// hd_kernels.hip -- gfx950 kernels of the flux-only discrete-ordinate solve.
+//
+//   hd_planck_kernel     one lane per (solve, level): Planck radiance of every
+//                        level + surface + top emission   [cdisort c_planck_func1]
+//   hd_layer_kernel<NN>  one lane per (solve, layer): delta-M, phase-matrix
+//                        assembly, symmetric eigenproblem (Cholesky + Jacobi),
+//                        beam/thermal particular solutions, and the layer's
+//                        reflection/transmission operators + sources in the
+//                        flux-weighted basis.   [c_setdis, c_soleig, c_upbeam,
+//                        c_upisot]
+//   hd_sweep_kernel<NN>  one lane per solve: adding sweep top->bottom,
+//                        Lambertian surface, back-substitution bottom->top,
+//                        level fluxes in harp layout.  [c_setmtx, c_solve0,
+//                        c_fluxes; pydisort gather + level reversal]
+//
+// Scratch layout per chunk (solve-interleaved: lane = solve, so every global
+// access of a wave is 64 consecutive doubles):
+//   planck      [L+3][nsc]       B(level 0..L, harp order), B(btemp), temis*B(ttemp)
+//   layer ops   [lc][NE1][nsc]   NE1 = NN(NN+1) + 2NN + 1
+//                                (R~ upper, T~ upper, S~+, S~-, tau')
+//   back-sub    [lc][NE2][nsc]   NE2 = NN^2 + 2NN + 1   (ZT, t, rc, cs)
+#include "hd_kernels.hpp"
+
+namespace hd {
+
+// quadrature tables for every NN, in the constant address space
+struct QuadTables {
+  Quad<1> q1;
+  Quad<2> q2;
+  Quad<3> q3;
+  Quad<4> q4;
+  Quad<5> q5;
+  Quad<6> q6;
+  Quad<7> q7;
+  Quad<8> q8;
+};
+__constant__ QuadTables c_quad;
+
+template <int NN>
+__device__ __forceinline__ const Quad<NN>& quad() {
+  if constexpr (NN == 1) return c_quad.q1;
+  else if constexpr (NN == 2) return c_quad.q2;
+  else if constexpr (NN == 3) return c_quad.q3;
+  else if constexpr (NN == 4) return c_quad.q4;
+  else if constexpr (NN == 5) return c_quad.q5;
+  else if constexpr (NN == 6) return c_quad.q6;
+  else if constexpr (NN == 7) return c_quad.q7;
+  else return c_quad.q8;
+}
+
+constexpr int kLayerBlock = 256;
+
+// ============================================================================
+// K0: Planck radiance per (solve, level)
+// ============================================================================
+__global__ __launch_bounds__(256) void hd_planck_kernel(PlanckArgs A) {
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int nl = A.nlyr + 3;
+  if (tid >= (long)A.nsc * nl) return;
+  const int lev = (int)(tid / A.nsc);
+  const int sl = (int)(tid - (long)lev * A.nsc);
+  const long s = A.s0 + sl;
+  const int w = (int)(s / A.ncol);
+  const int c = (int)(s - (long)w * A.ncol);
+  double b;
+  if (lev <= A.nlyr) {
+    b = plkavg(A.wlo[w], A.whi[w], A.temf[(size_t)c * (A.nlyr + 1) + lev]);
+  } else if (lev == A.nlyr + 1) {
+    b = plkavg(A.wlo[w], A.whi[w], A.btemp ? A.btemp[s] : 0.0);
+  } else {
+    const double te = A.temis ? A.temis[s] : 0.0;
+    b = te != 0.0 ? te * plkavg(A.wlo[w], A.whi[w], A.ttemp ? A.ttemp[s] : 0.0) : 0.0;
+  }
+  A.out[(size_t)lev * A.nsc + sl] = b;
+}
+
+// ============================================================================
+// K1: per-(solve, layer) setup
+// ============================================================================
+template <int NN>
+__global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
+  constexpr int N = 2 * NN;
+  constexpr int kPsi = NN > 1 ? NN * NN : 1;
+  __shared__ double psi_lds[kPsi * kLayerBlock];  // Psi^T staged per lane
+  const Quad<NN>& Qc = quad<NN>();
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long ntot = (long)A.nsc * A.nlyr;
+  if (tid >= ntot) return;
+  const int lt = threadIdx.x;
+  const int L = A.nlyr;
+  const int lc = (int)(tid / A.nsc);  // solver layer, 0 = top
+  const int sl = (int)(tid - (long)lc * A.nsc);
+  const long s = A.s0 + sl;
+  const int nm = A.nmom;
+  const int np = A.nprop;
+  int st = 0;
+
+  // ---- inputs of this layer (harp layer L-1-lc) + delta-M (c_setdis) ----
+  const double* q = A.prop + ((size_t)s * L + (L - 1 - lc)) * np;
+  const double tau = q[0];
+  double ssa = np > 1 ? q[1] : 0.0;
+  if (!(tau >= 0.0) || !(ssa >= 0.0) || !(ssa <= 1.0)) st |= kStBadInput;
+  if (ssa == 1.0) ssa = 1.0 - kDither;
+  const double f = nm >= N ? q[1 + N] : 0.0;
+  if (!(f < 1.0)) st |= kStBadInput;
+  const double taup = (1.0 - ssa * f) * tau;
+  const double om = ssa * (1.0 - f) / (1.0 - ssa * f);
+  const double rf = om / (1.0 - f);
+  double gl[N];
+#pragma unroll
+  for (int l = 0; l < N; ++l) {
+    const double chi = l == 0 ? 1.0 : (l <= nm ? q[1 + l] : 0.0);
+    gl[l] = (2 * l + 1) * (chi - f) * rf;
+  }
+
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
+  const double fb = A.fbeam ? A.fbeam[s] : 0.0;
+  const bool beam = fb > 0.0 && mu0 > 0.0;
+  if (beam && mu0 > 1.0) st |= kStBadInput;
+  const double rmu0 = beam ? 1.0 / mu0 : 0.0;
+
+  // ---- beam source vectors xs, xd (even/odd Legendre parts) ----
+  double xs[NN], xd[NN];
+  if (beam) {
+    double pl0[N];
+    pl0[0] = 1.0;
+    if (N > 1) pl0[1] = mu0;
+#pragma unroll
+    for (int l = 2; l < N; ++l)
+      pl0[l] = ((2 * l - 1) * mu0 * pl0[l - 1] - (l - 1) * pl0[l - 2]) * (1.0 / l);
+    const double fb2 = fb * (0.5 / kPi);
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      double se = 0.0, so = 0.0;
+#pragma unroll
+      for (int l = 0; l < N; ++l) {
+        const double t = gl[l] * pl0[l] * Qc.pt[l][i];
+        if (l % 2 == 0) se += t; else so += t;
+      }
+      xs[i] = fb2 * se;
+      xd[i] = -fb2 * so;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < NN; ++i) xs[i] = xd[i] = 0.0;
+  }
+
+  // ---- phase matrix even/odd parts -> -A- (lch), -A+ (ap), upper triangles ----
+  double lch[NN][NN], ap[NN][NN];
+#pragma unroll
+  for (int i = 0; i < NN; ++i) {
+#pragma unroll
+    for (int j = i; j < NN; ++j) {
+      double se = 0.0, so = 0.0;
+#pragma unroll
+      for (int l = 0; l < N; ++l) {
+        const double t = gl[l] * Qc.pt[l][i] * Qc.pt[l][j];
+        if (l % 2 == 0) se += t; else so += t;
+      }
+      const double diag = (i == j) ? 1.0 / Qc.mu[i] : 0.0;
+      const double sij = Qc.sd[i] * Qc.sd[j];
+      lch[i][j] = diag - sij * so;
+      ap[i][j] = diag - sij * se;
+    }
+  }
+  // L L^T = -A-  (lower triangle of lch)
+  if (!chol_inplace<NN>(lch)) st |= kStEigen;
+
+  // ---- pre-Jacobi vectors (depend on L only) ----
+  // beam: y2 = L^-1 W D^-1/2 rv, rv = -(M D^1/2)^-1 L L^T D^1/2 xs + M^-1 xd/mu0
+  //       lxd = D^1/2 L^-T L^-1 D^1/2 xd  (so that linv(xd) = lxd / w)
+  double y2[NN], lxd[NN];
+  if (beam) {
+    double y[NN], z[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) y[i] = Qc.sd[i] * xs[i];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {  // z = L^T y
+      double t = 0.0;
+#pragma unroll
+      for (int k = i; k < NN; ++k) t += lch[k][i] * y[k];
+      z[i] = t;
+    }
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {  // y = L z
+      double t = 0.0;
+#pragma unroll
+      for (int k = 0; k <= i; ++k) t += lch[i][k] * z[k];
+      y[i] = t;
+    }
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      const double rv = (-y[i] / Qc.sd[i] + xd[i] * rmu0) / Qc.mu[i];
+      y2[i] = Qc.w[i] / Qc.sd[i] * rv;
+      lxd[i] = Qc.sd[i] * xd[i];
+    }
+    lower_solve<NN>(lch, y2);
+    lower_solve<NN>(lch, lxd);
+    lower_t_solve<NN>(lch, lxd);
+#pragma unroll
+    for (int i = 0; i < NN; ++i) lxd[i] *= Qc.sd[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < NN; ++i) y2[i] = lxd[i] = 0.0;
+  }
+  // thermal: cvec = dB + 2 (dB/tau') h,  h = W^-1 D^1/2 L^-T L^-1 D^1/2 mu
+  double cvec[NN];
+  double db = 0.0, bsum = 0.0;
+  if (A.planck) {
+    const double bt = A.planckv[(size_t)(L - lc) * A.nsc + sl];
+    const double bb = A.planckv[(size_t)(L - lc - 1) * A.nsc + sl];
+    db = bb - bt;
+    bsum = bt + bb;
+    const double b1 = taup > 0.0 ? 2.0 * db / taup : 0.0;
+#pragma unroll
+    for (int i = 0; i < NN; ++i) cvec[i] = Qc.sd[i] * Qc.mu[i];
+    lower_solve<NN>(lch, cvec);
+    lower_t_solve<NN>(lch, cvec);
+#pragma unroll
+    for (int i = 0; i < NN; ++i) cvec[i] = db + b1 * Qc.sd[i] / Qc.w[i] * cvec[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < NN; ++i) cvec[i] = 0.0;
+  }
+
+  // ---- Sym = L^T (-A+) L (upper), built column by column ----
+  double sym[NN][NN];
+#pragma unroll
+  for (int j = 0; j < NN; ++j) {
+    double mcol[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      double t = 0.0;
+#pragma unroll
+      for (int k = j; k < NN; ++k) t += HD_SYM(ap, i, k) * lch[k][j];
+      mcol[i] = t;
+    }
+#pragma unroll
+    for (int i = 0; i <= j; ++i) {
+      double t = 0.0;
+#pragma unroll
+      for (int k = i; k < NN; ++k) t += lch[k][i] * mcol[k];
+      sym[i][j] = t;
+    }
+  }
+
+  // ---- eigenpairs (c_soleig): Sym = V diag(k^2) V^T ----
+  double v[NN][NN];
+  jacobi_eig<NN>(sym, v, A.max_sweeps);
+  double kk[NN];
+#pragma unroll
+  for (int j = 0; j < NN; ++j) {
+    const double k2 = sym[j][j];
+    if (!(k2 > 0.0)) st |= kStEigen;
+    kk[j] = sqrt(k2 > 0.0 ? k2 : 0.0);
+  }
+
+  // ---- beam particular solution Z+/- (c_upbeam), unit attenuation above ----
+  double zp[NN], zm[NN];
+  double e0 = 0.0;
+  if (beam) {
+    double tt[NN];
+    const double r2 = rmu0 * rmu0;
+#pragma unroll
+    for (int j = 0; j < NN; ++j) {  // tt = V^T y2 / (1/mu0^2 - k^2)
+      double t = 0.0;
+#pragma unroll
+      for (int i = 0; i < NN; ++i) t += v[i][j] * y2[i];
+      double den = r2 - kk[j] * kk[j];
+      if (fabs(den) < 1.0e-9 * r2) {
+        st |= kStResonance;
+        den = den < 0.0 ? -1.0e-9 * r2 : 1.0e-9 * r2;
+      }
+      tt[j] = t / den;
+    }
+    double sv[NN], y[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {  // y = V tt
+      double t = 0.0;
+#pragma unroll
+      for (int j = 0; j < NN; ++j) t += v[i][j] * tt[j];
+      y[i] = t;
+    }
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {  // s = W^-1 D^1/2 L y
+      double t = 0.0;
+#pragma unroll
+      for (int k = 0; k <= i; ++k) t += lch[i][k] * y[k];
+      sv[i] = Qc.sd[i] / Qc.w[i] * t;
+    }
+    // dd = linv(xd - mu s / mu0) = (lxd - D^1/2 L^-T L^-1 D^1/2 (mu s)/mu0) / w
+#pragma unroll
+    for (int i = 0; i < NN; ++i) y[i] = Qc.sd[i] * Qc.mu[i] * sv[i];
+    lower_solve<NN>(lch, y);
+    lower_t_solve<NN>(lch, y);
+    // cumulative scaled optical depth of the layers above
+    double tauc = 0.0;
+    for (int l2 = 0; l2 < lc; ++l2) {
+      const double* q2 = A.prop + ((size_t)s * L + (L - 1 - l2)) * np;
+      double a2 = np > 1 ? q2[1] : 0.0;
+      if (a2 == 1.0) a2 = 1.0 - kDither;
+      const double f2 = nm >= N ? q2[1 + N] : 0.0;
+      tauc += (1.0 - a2 * f2) * q2[0];
+    }
+    const double att = 0.5 * exp(-tauc * rmu0);
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      const double dd = (lxd[i] - Qc.sd[i] * y[i] * rmu0) / Qc.w[i];
+      zp[i] = (sv[i] + dd) * att;
+      zm[i] = (sv[i] - dd) * att;
+    }
+    e0 = exp(-taup * rmu0);
+  } else {
+#pragma unroll
+    for (int i = 0; i < NN; ++i) zp[i] = zm[i] = 0.0;
+  }
+
+  // ---- layer operators in the flux-weighted basis ----
+  // Delta = tanh(k tau'/2)/k, Gamma = k tanh(k tau'/2)
+  double dsq[NN], gsq[NN];
+#pragma unroll
+  for (int j = 0; j < NN; ++j) {
+    const double x = kk[j] * taup;
+    const double e = exp(-x);
+    const double m = -expm1(-x);
+    const double th = m / (1.0 + e);
+    const double delta = x > 1.0e-8 ? th / kk[j] : 0.5 * taup;
+    dsq[j] = sqrt(delta);
+    gsq[j] = sqrt(kk[j] * th);
+  }
+  // Psi^T = L^-T V Gamma^1/2 -> LDS (one column of 8 doubles per lane at a time)
+#pragma unroll
+  for (int j = 0; j < NN; ++j) {
+    double x[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) x[i] = v[i][j];
+    lower_t_solve<NN>(lch, x);
+#pragma unroll
+    for (int i = 0; i < NN; ++i) psi_lds[(i * NN + j) * kLayerBlock + lt] = x[i] * gsq[j];
+  }
+  // Omega = L V Delta^1/2, in place over v (rows bottom-up)
+#pragma unroll
+  for (int i = NN - 1; i >= 0; --i)
+#pragma unroll
+    for (int j = 0; j < NN; ++j) {
+      double t = 0.0;
+#pragma unroll
+      for (int a = 0; a <= i; ++a) t += lch[i][a] * v[a][j];
+      v[i][j] = t * dsq[j];
+    }
+
+  double* out = A.scr + (size_t)lc * ne1<NN>() * A.nsc + sl;
+  const size_t so = A.nsc;
+  constexpr int nsym = NN * (NN + 1) / 2;
+  double ga[NN], gb[NN];
+#pragma unroll
+  for (int i = 0; i < NN; ++i) {
+    ga[i] = Qc.g[i] * (cvec[i] - (zm[i] - zp[i] * e0));
+    gb[i] = Qc.g[i] * (zm[i] + zp[i] * e0 + bsum);
+  }
+  // Q~- = Omega (I + Omega^T Omega)^-1 Omega^T = Phi Phi^T, Phi = Omega J^-T
+  double pvec[NN];
+  {
+    double hm[NN][NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int j = i; j < NN; ++j) {
+        double t = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < NN; ++k) t += v[k][i] * v[k][j];
+        hm[i][j] = t;
+      }
+    if (!chol_inplace<NN>(hm)) st |= kStEigen;
+#pragma unroll
+    for (int r = 0; r < NN; ++r) lower_solve<NN>(hm, v[r]);
+    // Q~- (upper) -> temporarily into the R~ slot; p = Q~- ga
+#pragma unroll
+    for (int i = 0; i < NN; ++i) pvec[i] = 0.0;
+    int e = 0;
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int j = i; j < NN; ++j) {
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < NN; ++k) t += v[i][k] * v[j][k];
+        out[(e++) * so] = t;
+        pvec[i] += t * ga[j];
+        if (j != i) pvec[j] += t * ga[i];
+      }
+  }
+  // Q~+ = -Psi^T (I + Psi Psi^T)^-1 Psi = -Xi^T Xi, Xi = J+^-1 Psi
+  double qp[NN][NN];
+  {
+    double pt_[NN][NN];  // pt_[i][j] = Psi^T[i][j]
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int j = 0; j < NN; ++j) pt_[i][j] = psi_lds[(i * NN + j) * kLayerBlock + lt];
+    double hp[NN][NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int j = i; j < NN; ++j) {
+        double t = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < NN; ++k) t += pt_[k][i] * pt_[k][j];
+        hp[i][j] = t;
+      }
+    if (!chol_inplace<NN>(hp)) st |= kStEigen;
+#pragma unroll
+    for (int r = 0; r < NN; ++r) lower_solve<NN>(hp, pt_[r]);
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int j = i; j < NN; ++j) {
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < NN; ++k) t += pt_[i][k] * pt_[j][k];
+        qp[i][j] = -t;
+      }
+  }
+  double qvec[NN];
+#pragma unroll
+  for (int i = 0; i < NN; ++i) {
+    double t = 0.0;
+#pragma unroll
+    for (int j = 0; j < NN; ++j) t += HD_SYM(qp, i, j) * gb[j];
+    qvec[i] = t;
+  }
+
+  // ---- store: R~ = Q~- + Q~+, T~ = I - Q~- + Q~+ (upper), S~+, S~-, tau' ----
+  double chk = 0.0;
+  {
+    int e = 0;
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int j = i; j < NN; ++j) {
+        const double qm = out[e * so];
+        const double r = qm + qp[i][j];
+        const double t = ((i == j) ? 1.0 : 0.0) - qm + qp[i][j];
+        out[e * so] = r;
+        out[(nsym + e) * so] = t;
+        chk += r + t;
+        ++e;
+      }
+  }
+#pragma unroll
+  for (int i = 0; i < NN; ++i) {
+    const double sp = Qc.g[i] * (zp[i] * (1.0 - e0) - db) + pvec[i] - qvec[i];
+    const double sm = Qc.g[i] * (-zm[i] * (1.0 - e0) + db) - pvec[i] - qvec[i];
+    out[(2 * nsym + i) * so] = sp;
+    out[(2 * nsym + NN + i) * so] = sm;
+    chk += sp + sm;
+  }
+  out[(2 * nsym + 2 * NN) * so] = taup;
+  if (!isfinite(chk + taup)) st |= kStNonFinite;
+  if (st) {
+    atomicOr(&A.status[s], st);
+    if (st & 0x0F) atomicOr(A.anyerr, 1);
+  }
+}
+
+// ============================================================================
+// K2: per-solve adding sweep + back-substitution
+// ============================================================================
+template <int NN>
+__global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
+  const Quad<NN>& Qc = quad<NN>();
+  const long sl = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (sl >= A.nsc) return;
+  const long s = A.s0 + sl;
+  const int L = A.nlyr;
+  const size_t nsc = A.nsc;
+  constexpr int nsym = NN * (NN + 1) / 2;
+  int st = 0;
+
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
+  const double fb = A.fbeam ? A.fbeam[s] : 0.0;
+  const bool beam = fb > 0.0 && mu0 > 0.0;
+  const double alb = A.albedo ? A.albedo[s] : 0.0;
+  if (!(alb >= 0.0) || !(alb <= 1.0)) st |= kStBadInput;
+  double top = A.fisot ? A.fisot[s] : 0.0;
+  double bsurf = 0.0;
+  if (A.planck) {
+    bsurf = A.planckv[(size_t)(L + 1) * nsc + sl];
+    top += A.planckv[(size_t)(L + 2) * nsc + sl];
+  }
+  const double twopi = 2.0 * kPi;
+  const double rmu0 = beam ? 1.0 / mu0 : 0.0;
+  const double f0mu0 = beam ? fb * mu0 : 0.0;
+
+  double ra[NN][NN];  // reflection of the stack above (upper triangle)
+  double sd[NN];      // diffuse downward source at the current interface
+#pragma unroll
+  for (int i = 0; i < NN; ++i) {
+    sd[i] = Qc.g[i] * top;
+#pragma unroll
+    for (int j = i; j < NN; ++j) ra[i][j] = 0.0;
+  }
+  double tauc = 0.0;
+
+  for (int lc = 0; lc < L; ++lc) {
+    const double* lp = A.scr + (size_t)lc * ne1<NN>() * nsc + sl;
+    double* bp = A.bsub + (size_t)lc * ne2<NN>() * nsc + sl;
+#define RL(i, j) lp[(size_t)sym_index<NN>(i, j) * nsc]
+#define TL(i, j) lp[(size_t)(nsym + sym_index<NN>(i, j)) * nsc]
+
+    // level lc (top of layer lc): F_dn = rc . I+ + cs
+    {
+      double cs = 0.0;
+#pragma unroll
+      for (int i = 0; i < NN; ++i) {
+        double t = 0.0;
+#pragma unroll
+        for (int j = 0; j < NN; ++j) t += HD_SYM(ra, j, i) * Qc.g[j];
+        bp[(NN * NN + NN + i) * nsc] = twopi * t;
+        cs += Qc.g[i] * sd[i];
+      }
+      bp[(NN * NN + 2 * NN) * nsc] = twopi * cs + f0mu0 * exp(-tauc * rmu0);
+    }
+
+    // A = Ra (full); W1 = I - R_l A ; v1 = R_l Sd + S+
+    double am[NN][NN], w1[NN][NN], t1[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int j = 0; j < NN; ++j) am[i][j] = HD_SYM(ra, i, j);
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      double rrow[NN];
+#pragma unroll
+      for (int k = 0; k < NN; ++k) rrow[k] = RL(i, k);
+#pragma unroll
+      for (int j = 0; j < NN; ++j) {
+        double t = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < NN; ++k) t -= rrow[k] * am[k][j];
+        w1[i][j] = t;
+      }
+      double t = lp[(2 * nsym + i) * nsc];
+#pragma unroll
+      for (int k = 0; k < NN; ++k) t += rrow[k] * sd[k];
+      t1[i] = t;
+    }
+    // LU without pivoting (W1 = I - product of reflections; pivot watch)
+#pragma unroll
+    for (int k = 0; k < NN; ++k) {
+      const double piv = w1[k][k];
+      if (!(fabs(piv) > 1.0e-12)) st |= kStPivot;
+      const double rp = 1.0 / piv;
+      w1[k][k] = rp;  // reciprocal kept on the diagonal
+#pragma unroll
+      for (int i = k + 1; i < NN; ++i) {
+        const double l = w1[i][k] * rp;
+        w1[i][k] = l;
+#pragma unroll
+        for (int j = k + 1; j < NN; ++j) w1[i][j] -= l * w1[k][j];
+      }
+    }
+    // t = W1^-1 v1
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int k = 0; k < i; ++k) t1[i] -= w1[i][k] * t1[k];
+#pragma unroll
+    for (int i = NN - 1; i >= 0; --i) {
+#pragma unroll
+      for (int k = i + 1; k < NN; ++k) t1[i] -= w1[i][k] * t1[k];
+      t1[i] *= w1[i][i];
+    }
+    // u = A t + Sd
+    double u[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      double t = sd[i];
+#pragma unroll
+      for (int k = 0; k < NN; ++k) t += am[i][k] * t1[k];
+      u[i] = t;
+      bp[(NN * NN + i) * nsc] = t1[i];
+    }
+    // M1 = A W1^-1, row-wise in place:  x W1 = a  ->  (x L) U = a
+#pragma unroll
+    for (int r = 0; r < NN; ++r) {
+#pragma unroll
+      for (int j = 0; j < NN; ++j) {  // z U = a  (forward over columns)
+        double t = am[r][j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) t -= am[r][k] * w1[k][j];
+        am[r][j] = t * w1[j][j];
+      }
+#pragma unroll
+      for (int j = NN - 1; j >= 0; --j) {  // x L = z  (backward, unit L)
+        double t = am[r][j];
+#pragma unroll
+        for (int k = j + 1; k < NN; ++k) t -= am[r][k] * w1[k][j];
+        am[r][j] = t;
+      }
+    }
+    // ZT = W1^-1 T_l (stored column by column)
+#pragma unroll
+    for (int j = 0; j < NN; ++j) {
+      double x[NN];
+#pragma unroll
+      for (int i = 0; i < NN; ++i) x[i] = TL(i, j);
+#pragma unroll
+      for (int i = 0; i < NN; ++i)
+#pragma unroll
+        for (int k = 0; k < i; ++k) x[i] -= w1[i][k] * x[k];
+#pragma unroll
+      for (int i = NN - 1; i >= 0; --i) {
+#pragma unroll
+        for (int k = i + 1; k < NN; ++k) x[i] -= w1[i][k] * x[k];
+        x[i] *= w1[i][i];
+      }
+#pragma unroll
+      for (int i = 0; i < NN; ++i) bp[(i * NN + j) * nsc] = x[i];
+    }
+    // P = M1 T_l (row-wise in place)
+    double tl[NN][NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int j = i; j < NN; ++j) tl[i][j] = TL(i, j);
+#pragma unroll
+    for (int r = 0; r < NN; ++r) {
+      double row[NN];
+#pragma unroll
+      for (int j = 0; j < NN; ++j) {
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < NN; ++k) t += am[r][k] * HD_SYM(tl, k, j);
+        row[j] = t;
+      }
+#pragma unroll
+      for (int j = 0; j < NN; ++j) am[r][j] = row[j];
+    }
+    // Ra <- R_l + T_l P (upper) ; Sd <- T_l u + S-
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+#pragma unroll
+      for (int j = i; j < NN; ++j) {
+        double t = RL(i, j);
+#pragma unroll
+        for (int k = 0; k < NN; ++k) t += HD_SYM(tl, i, k) * am[k][j];
+        ra[i][j] = t;
+      }
+      double t = lp[(2 * nsym + NN + i) * nsc];
+#pragma unroll
+      for (int k = 0; k < NN; ++k) t += HD_SYM(tl, i, k) * u[k];
+      sd[i] = t;
+    }
+    tauc += lp[(2 * nsym + 2 * NN) * nsc];
+#undef RL
+#undef TL
+  }
+
+  // ---- Lambertian surface: I+ = g x ----
+  double gsd = 0.0, grg = 0.0;
+#pragma unroll
+  for (int i = 0; i < NN; ++i) {
+    gsd += Qc.g[i] * sd[i];
+#pragma unroll
+    for (int j = 0; j < NN; ++j) grg += Qc.g[i] * HD_SYM(ra, i, j) * Qc.g[j];
+  }
+  double esurf = (1.0 - alb) * bsurf;
+  const double dirsurf = f0mu0 * exp(-tauc * rmu0);
+  if (beam) esurf += alb * dirsurf / kPi;
+  const double x = (2.0 * alb * gsd + esurf) / (1.0 - 2.0 * alb * grg);
+  double ip[NN];
+#pragma unroll
+  for (int i = 0; i < NN; ++i) ip[i] = Qc.g[i] * x;
+  double* fo = A.flux + (size_t)s * (L + 1) * 2;
+  double chk = 0.0;
+  {
+    double up = 0.0, dn = 0.0;
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      up += Qc.g[i] * ip[i];
+      double t = sd[i];
+#pragma unroll
+      for (int j = 0; j < NN; ++j) t += HD_SYM(ra, i, j) * ip[j];
+      dn += Qc.g[i] * t;
+    }
+    fo[0] = twopi * up;
+    fo[1] = twopi * dn + dirsurf;
+    chk += fo[0] + fo[1];
+  }
+  // ---- back-substitution bottom -> top ----
+  for (int lc = L - 1; lc >= 0; --lc) {
+    const double* bp = A.bsub + (size_t)lc * ne2<NN>() * nsc + sl;
+    double nip[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      double t = bp[(NN * NN + i) * nsc];
+#pragma unroll
+      for (int j = 0; j < NN; ++j) t += bp[(i * NN + j) * nsc] * ip[j];
+      nip[i] = t;
+    }
+    double up = 0.0, dn = bp[(NN * NN + 2 * NN) * nsc];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      ip[i] = nip[i];
+      up += Qc.g[i] * nip[i];
+      dn += bp[(NN * NN + NN + i) * nsc] * nip[i];
+    }
+    const int lev = L - lc;
+    fo[2 * lev] = twopi * up;
+    fo[2 * lev + 1] = dn;
+    chk += fo[2 * lev] + fo[2 * lev + 1];
+  }
+  if (!isfinite(chk)) st |= kStNonFinite;
+  if (st) {
+    atomicOr(&A.status[s], st);
+    if (st & 0x0F) atomicOr(A.anyerr, 1);
+  }
+}
+
+// ============================================================================
+// host side: constant tables + launchers
+// ============================================================================
+template <int NN>
+static void fill_quad(Quad<NN>& q, const QuadHost& h) {
+  for (int i = 0; i < NN; ++i) {
+    q.mu[i] = h.mu[i];
+    q.w[i] = h.w[i];
+    q.sd[i] = h.sd[i];
+    q.g[i] = h.g[i];
+    for (int l = 0; l < 2 * NN; ++l) q.pt[l][i] = h.pt[l][i];
+  }
+}
+
+hipError_t upload_quad_tables(const QuadHost* per_nn /* [kMaxNN], index nn-1 */) {
+  QuadTables t;
+  fill_quad<1>(t.q1, per_nn[0]);
+  fill_quad<2>(t.q2, per_nn[1]);
+  fill_quad<3>(t.q3, per_nn[2]);
+  fill_quad<4>(t.q4, per_nn[3]);
+  fill_quad<5>(t.q5, per_nn[4]);
+  fill_quad<6>(t.q6, per_nn[5]);
+  fill_quad<7>(t.q7, per_nn[6]);
+  fill_quad<8>(t.q8, per_nn[7]);
+  return hipMemcpyToSymbol(HIP_SYMBOL(c_quad), &t, sizeof(t), 0, hipMemcpyHostToDevice);
+}
+
+template <int NN>
+static hipError_t launch_chunk(const PlanckArgs* pa, const LayerArgs& la, const SweepArgs& sa,
+                               hipStream_t stream, hipEvent_t* ev) {
+  if (pa) {
+    const long n0 = (long)pa->nsc * (pa->nlyr + 3);
+    hipLaunchKernelGGL(hd_planck_kernel, dim3((unsigned)((n0 + 255) / 256)), dim3(256), 0,
+                       stream, *pa);
+  }
+  const long ntot = (long)la.nsc * la.nlyr;
+  const unsigned nb1 = (unsigned)((ntot + kLayerBlock - 1) / kLayerBlock);
+  const unsigned nb2 = (unsigned)((la.nsc + 63) / 64);
+  if (ev) (void)hipEventRecord(ev[0], stream);
+  hipLaunchKernelGGL(hd_layer_kernel<NN>, dim3(nb1), dim3(kLayerBlock), 0, stream, la);
+  if (ev) (void)hipEventRecord(ev[1], stream);
+  hipLaunchKernelGGL(hd_sweep_kernel<NN>, dim3(nb2), dim3(64), 0, stream, sa);
+  if (ev) (void)hipEventRecord(ev[2], stream);
+  return hipGetLastError();
+}
+
+hipError_t launch_solve_chunk_nn(int nn, const PlanckArgs* pa, const LayerArgs& la,
+                                 const SweepArgs& sa, hipStream_t stream, hipEvent_t* ev) {
+  switch (nn) {
+    case 1: return launch_chunk<1>(pa, la, sa, stream, ev);
+    case 2: return launch_chunk<2>(pa, la, sa, stream, ev);
+    case 3: return launch_chunk<3>(pa, la, sa, stream, ev);
+    case 4: return launch_chunk<4>(pa, la, sa, stream, ev);
+    case 5: return launch_chunk<5>(pa, la, sa, stream, ev);
+    case 6: return launch_chunk<6>(pa, la, sa, stream, ev);
+    case 7: return launch_chunk<7>(pa, la, sa, stream, ev);
+    case 8: return launch_chunk<8>(pa, la, sa, stream, ev);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+size_t scratch_doubles_per_solve(int nn, int nlyr, bool planck) {
+  const size_t ne1 = (size_t)(nn * (nn + 1) + 2 * nn + 1);
+  const size_t ne2 = (size_t)(nn * nn + 2 * nn + 1);
+  return (ne1 + ne2) * nlyr + (planck ? (size_t)nlyr + 3 : 0);
+}
+
+}  // namespace hd

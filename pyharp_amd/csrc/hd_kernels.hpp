@@ -1,0 +1,88 @@
+// hd_kernels.hpp -- kernel argument blocks and launcher declarations.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "hd_device.hpp"
+
+namespace hd {
+
+constexpr int kMaxNN = 8;  // nstr <= 16 in this release
+
+template <int NN>
+__host__ __device__ constexpr int ne1() {  // per-layer operator record (doubles)
+  return NN * (NN + 1) + 2 * NN + 1;
+}
+template <int NN>
+__host__ __device__ constexpr int ne2() {  // per-level back-substitution record
+  return NN * NN + 2 * NN + 1;
+}
+// packed row-major upper-triangle index of (i, j) in either order
+template <int NN>
+__host__ __device__ constexpr int sym_index(int i, int j) {
+  return i <= j ? i * NN - i * (i - 1) / 2 + (j - i) : j * NN - j * (j - 1) / 2 + (i - j);
+}
+
+struct PlanckArgs {
+  const double* temf;   // [ncol][nlyr+1], level 0 = bottom
+  const double* btemp;  // [S] or null
+  const double* ttemp;  // [S] or null
+  const double* temis;  // [S] or null
+  const double* wlo;    // [nwave]
+  const double* whi;    // [nwave]
+  double* out;          // [nlyr+3][nsc]
+  long s0;
+  int nsc;
+  int ncol;
+  int nlyr;
+};
+
+struct LayerArgs {
+  const double* prop;
+  const double* fbeam;
+  const double* umu0;
+  const double* planckv;  // [nlyr+3][nsc] (planck) or null
+  double* scr;
+  int* status;
+  int* anyerr;
+  long s0;    // first solve of this chunk (flattened wave*ncol + col)
+  int nsc;    // solves in this chunk (= scratch stride)
+  int ncol;
+  int nlyr;
+  int nprop;
+  int nmom;   // moments used = min(nmom, nprop-2)
+  int planck;
+  int max_sweeps;
+};
+
+struct SweepArgs {
+  const double* scr;
+  double* bsub;
+  double* flux;
+  const double* fbeam;
+  const double* umu0;
+  const double* albedo;
+  const double* fisot;
+  const double* planckv;
+  int* status;
+  int* anyerr;
+  long s0;
+  int nsc;
+  int ncol;
+  int nlyr;
+  int planck;
+};
+
+struct QuadHost {
+  double mu[kMaxNN], w[kMaxNN], sd[kMaxNN], g[kMaxNN];
+  double pt[2 * kMaxNN][kMaxNN];
+};
+
+// copy the quadrature tables (index nn-1) into the current device's constant memory
+hipError_t upload_quad_tables(const QuadHost* per_nn);
+// ev: 3 events (before K1, between, after K2) or nullptr; pa null when planck is off
+hipError_t launch_solve_chunk_nn(int nn, const PlanckArgs* pa, const LayerArgs& la,
+                                 const SweepArgs& sa, hipStream_t stream, hipEvent_t* ev);
+size_t scratch_doubles_per_solve(int nn, int nlyr, bool planck);
+
+}  // namespace hd

@@ -1,0 +1,220 @@
+"""Drop-in DISORT flux module (pydisort ``disort::Disort`` contract) on MI355X.
+
+Mirrors the API pyharp uses at its call sites
+(``examples/amars_sw.cpp:43-65,216,280``, ``examples/amars_lw.cpp:18-38,60,80``,
+``tests/test_disort.cpp:13-55``, ``src/radiation/radiation_band.cpp:57-69,123-128``)::
+
+    op = DisortOptions().header("...").flags("lamber,quiet,onlyfl")
+    op.nwave(500).ncol(1)
+    op.ds().nlyr = 40; op.ds().nstr = 8; op.ds().nmom = 8
+    disort = Disort(op)
+    flux = disort.forward(prop, bc)            # or forward(prop, bc, temf)
+
+``prop`` (nwave, ncol, nlyr, nprop) f64, layer 0 = bottom; ``bc`` dict of
+(nwave, ncol) tensors; ``temf`` (ncol, nlyr+1) level temperatures bottom->top.
+Returns ``flux`` (nwave, ncol, nlyr+1, 2): level 0 = surface, [...,0] upward,
+[...,1] downward (rfldir + rfldn).  CPU tensors are staged through the GPU and
+the result is returned on the input's device; CUDA tensors stay on device.
+
+The arithmetic runs in libhdisort.so (HIP, gfx950) through the C-ABI in
+include/hdisort.h.  There is no CPU fallback: without a HIP device or without
+the built library, ``forward`` raises.
+"""
+
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+
+from . import _lib
+from .index import IEX, ISS, IPM  # noqa: F401  (re-exported like disort::index)
+from .rtsolver import RTSolver
+
+_KNOWN_FLAGS = {
+    "lamber", "quiet", "onlyfl", "planck", "usrtau", "usrang", "intensity_correction",
+    "old_intensity_correction", "print-input", "print-fluxes", "print-intensity",
+    "print-transmissivity", "print-phase-function", "deltam", "lyrcut", "ibcnd",
+}
+_BC_KEYS = ("fbeam", "umu0", "albedo", "btemp", "ttemp", "temis", "fisot")
+_BC_IGNORED = ("phi0",)  # azimuth of the beam: no effect on m=0 fluxes
+
+
+class _DisortState:
+    """Subset of cdisort's disort_state exposed by ``DisortOptions.ds()``."""
+
+    def __init__(self):
+        self.nlyr = 1
+        self.nstr = 4
+        self.nmom = 4
+        self.nphi = 0
+        self.ntau = 0
+        self.numu = 0
+        self.utau = []
+
+    def __repr__(self):
+        return (f"disort_state(nlyr={self.nlyr}, nstr={self.nstr}, nmom={self.nmom}, "
+                f"nphi={self.nphi}, ntau={self.ntau}, numu={self.numu})")
+
+
+def _arg(name, default):
+    """harp ADD_ARG idiom: obj.name(value) sets and returns obj; obj.name() reads."""
+
+    def accessor(self, *value):
+        if value:
+            setattr(self, "_" + name, value[0])
+            return self
+        return getattr(self, "_" + name, default() if callable(default) else default)
+
+    accessor.__name__ = name
+    return accessor
+
+
+class DisortOptions:
+    header = _arg("header", "")
+    flags = _arg("flags", "")
+    nwave = _arg("nwave", 1)
+    ncol = _arg("ncol", 1)
+    wave_lower = _arg("wave_lower", list)
+    wave_upper = _arg("wave_upper", list)
+    user_tau = _arg("user_tau", list)
+    user_mu = _arg("user_mu", list)
+    user_phi = _arg("user_phi", list)
+    device = _arg("device", 0)
+
+    def __init__(self):
+        self._ds = _DisortState()
+
+    def ds(self) -> _DisortState:
+        return self._ds
+
+    def flag_set(self) -> set:
+        return {f.strip() for f in self.flags().split(",") if f.strip()}
+
+    def __repr__(self):
+        return (f"DisortOptions(flags='{self.flags()}', nwave={self.nwave()}, "
+                f"ncol={self.ncol()}, ds={self._ds})")
+
+
+_CONTEXTS: Dict[int, _lib.Context] = {}
+
+
+def _context(device: int) -> _lib.Context:
+    ctx = _CONTEXTS.get(device)
+    if ctx is None:
+        ctx = _lib.Context(device)
+        _CONTEXTS[device] = ctx
+    return ctx
+
+
+class Disort(RTSolver):
+    """MI355X flux-only DISORT module (drop-in for pydisort's DisortImpl)."""
+
+    def __init__(self, options: Optional[DisortOptions] = None):
+        self.options = options if options is not None else DisortOptions()
+        self.reset()
+
+    def reset(self):
+        op = self.options
+        flags = op.flag_set()
+        unknown = flags - _KNOWN_FLAGS
+        if unknown:
+            raise RuntimeError(f"Disort: unknown flags {sorted(unknown)}")
+        ds = op.ds()
+        if ds.nstr < 2 or ds.nstr % 2 or ds.nstr > 16:
+            raise RuntimeError(f"Disort: nstr={ds.nstr} must be even and in [2, 16]")
+        if ds.nlyr < 1:
+            raise RuntimeError(f"Disort: nlyr={ds.nlyr} must be >= 1")
+        if "lamber" not in flags:
+            raise RuntimeError("Disort: only Lambertian lower boundaries are supported "
+                               "(set the 'lamber' flag)")
+        self.planck = "planck" in flags
+        if self.planck:
+            if len(op.wave_lower()) != op.nwave() or len(op.wave_upper()) != op.nwave():
+                raise RuntimeError("Disort: planck needs wave_lower/wave_upper of size nwave")
+
+    def ds(self):
+        return self.options.ds()
+
+    def get_rad(self, *args, **kwargs):
+        raise NotImplementedError("Disort.get_rad: the intensity path (usrang/usrtau "
+                                  "radiances) is not part of this flux-only solver")
+
+    # ------------------------------------------------------------------ #
+    def forward(self, prop: torch.Tensor, bc: Optional[Dict[str, torch.Tensor]] = None,
+                temf: Optional[torch.Tensor] = None, *, status: Optional[torch.Tensor] = None,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        op = self.options
+        ds = op.ds()
+        bc = {} if bc is None else bc
+        if prop.dim() != 4:
+            raise RuntimeError(f"Disort.forward: prop must be (nwave, ncol, nlyr, nprop), got "
+                               f"{tuple(prop.shape)}")
+        nwave, ncol, nlyr, nprop = prop.shape
+        if nlyr != ds.nlyr:
+            raise RuntimeError(f"Disort.forward: prop has {nlyr} layers, ds().nlyr = {ds.nlyr}")
+        for k in bc:
+            if k not in _BC_KEYS and k not in _BC_IGNORED:
+                raise RuntimeError(f"Disort.forward: unknown boundary condition '{k}'")
+        if self.planck and temf is None:
+            raise RuntimeError("Disort.forward: planck flag set but temf not given")
+        if not torch.cuda.is_available():
+            raise RuntimeError("Disort.forward: no HIP device available (pyharp_amd has no "
+                               "CPU path)")
+        in_dev = prop.device
+        dev = in_dev if in_dev.type == "cuda" else torch.device("cuda", int(op.device()))
+        f64 = torch.float64
+
+        def dev_tensor(x, shape=None):
+            if x is None:
+                return None
+            t = torch.as_tensor(x, dtype=f64)
+            if shape is not None:
+                t = t.expand(shape) if t.dim() < len(shape) or t.shape != shape else t
+            return t.to(dev).contiguous()
+
+        p = dev_tensor(prop)
+        keep = [p]
+        bct = {}
+        for k in _BC_KEYS:
+            if k in bc and bc[k] is not None:
+                t = dev_tensor(bc[k], (nwave, ncol))
+                if tuple(t.shape) != (nwave, ncol):
+                    raise RuntimeError(f"Disort.forward: bc['{k}'] must be (nwave, ncol)")
+                bct[k] = t
+                keep.append(t)
+        tf = wl = wu = None
+        if self.planck:
+            tf = dev_tensor(temf)
+            if tuple(tf.shape) != (ncol, nlyr + 1):
+                raise RuntimeError(f"Disort.forward: temf must be (ncol, nlyr+1) = "
+                                   f"{(ncol, nlyr + 1)}, got {tuple(tf.shape)}")
+            wl = torch.tensor(op.wave_lower(), dtype=f64, device=dev)
+            wu = torch.tensor(op.wave_upper(), dtype=f64, device=dev)
+            keep += [tf, wl, wu]
+        if out is None or out.device != dev:
+            flux = torch.empty((nwave, ncol, nlyr + 1, 2), dtype=f64, device=dev)
+        else:
+            flux = out
+
+        def ptr(t):
+            return t.data_ptr() if t is not None else None
+
+        cfg = _lib.HdConfig(nstr=ds.nstr, nmom=ds.nmom, nlyr=nlyr, nprop=nprop,
+                            flags=_lib.HD_FLAG_LAMBER | _lib.HD_FLAG_ONLYFL |
+                            (_lib.HD_FLAG_PLANCK if self.planck else 0))
+        inp = _lib.HdInputs(nwave=nwave, ncol=ncol, prop=ptr(p),
+                            fbeam=ptr(bct.get("fbeam")), umu0=ptr(bct.get("umu0")),
+                            albedo=ptr(bct.get("albedo")), btemp=ptr(bct.get("btemp")),
+                            ttemp=ptr(bct.get("ttemp")), temis=ptr(bct.get("temis")),
+                            fisot=ptr(bct.get("fisot")), temf=ptr(tf), wave_lower=ptr(wl),
+                            wave_upper=ptr(wu))
+        stream = torch.cuda.current_stream(dev)
+        with torch.cuda.device(dev):
+            _context(dev.index).solve(cfg, inp, flux.data_ptr(),
+                                      status.data_ptr() if status is not None else None,
+                                      stream.cuda_stream)
+        del keep
+        if in_dev.type != "cuda":
+            return flux.to(in_dev)
+        return flux

@@ -47,55 +47,66 @@ def layer_ops(dtau, ssa, chi, nstr, umu0, fbeam, b_top, b_bot, tauc_top):
     sym = lch.T @ ap @ lch
     k2, v = np.linalg.eigh(sym)
     k = np.sqrt(k2)
-    lv = lch @ v
-    x = (sd / w)[:, None] * lv
-    y = -(sd / w)[:, None] * np.linalg.solve(lch.T, v) * k[None, :]
+    # ---- layer operators in the flux-weighted basis (g = sqrt(w mu)) ----
     e = np.exp(-k * taup)
     m = -np.expm1(-k * taup)
-    dp = x * (1 + e) - y * m
-    dm = x * m - y * (1 + e)
-    qm = np.linalg.solve(dm.T, (x * m).T).T
-    qp = np.linalg.solve(dp.T, (y * m).T).T
-    r = qm + qp
-    t = np.eye(nn) - qm + qp
+    th = m / (1.0 + e)                        # tanh(k tau'/2)
+    delta = np.where(k * taup > 1e-8, th / np.where(k > 0, k, 1.0), 0.5 * taup)
+    gamma = k * th
+    u = lch @ v                               # U = L V
+    omega = u * np.sqrt(delta)[None, :]       # Omega = U Delta^1/2
+    psit = np.linalg.solve(lch.T, v) * np.sqrt(gamma)[None, :]   # Psi^T = L^-T V Gamma^1/2
+    hm = np.eye(nn) + omega.T @ omega
+    jm = np.linalg.cholesky(hm)
+    phi = np.linalg.solve(jm, omega.T).T      # Omega J^-T
+    qtm = phi @ phi.T                         # Q~- = Omega (I + Omega^T Omega)^-1 Omega^T
+    hp = np.eye(nn) + psit.T @ psit           # I + Psi Psi^T
+    jp = np.linalg.cholesky(hp)
+    xi = np.linalg.solve(jp, psit.T)          # J^-1 Psi
+    qtp = -(xi.T @ xi)                        # Q~+ = -Psi^T (I + Psi Psi^T)^-1 Psi
+    g = np.sqrt(w * mu)
+    rt = qtm + qtp                            # R~ (symmetric)
+    tt_ = np.eye(nn) - qtm + qtp              # T~ (symmetric)
 
     def linv(vec):   # W^-1 D^1/2 L^-T L^-1 D^1/2 vec
         z = np.linalg.solve(lch, sd * vec)
         z = np.linalg.solve(lch.T, z)
         return sd * z / w
 
-    splus_src = np.zeros(nn)
-    sminus_src = np.zeros(nn)
+    zp = np.zeros(nn)
+    zm = np.zeros(nn)
     e0 = 1.0
     if fbeam > 0 and umu0 > 0:
         e0 = math.exp(-taup / umu0)
         p0 = legendre_table(nstr, [umu0])[:, 0]
         xs = fbeam / (2 * math.pi) * (pt[ev].T @ (gl[ev] * p0[ev]))
         xd = -fbeam / (2 * math.pi) * (pt[~ev].T @ (gl[~ev] * p0[~ev]))
-        # r = (alpha-beta) M^-1 xs + M^-1 xd / mu0 ; (alpha-beta)M^-1 = -M^-1 D^-1/2 L L^T D^1/2
         rv = -(1.0 / (mu * sd)) * (lch @ (lch.T @ (sd * xs))) + xd / (mu * umu0)
-        # X^-1 = V^T L^-1 D^-1/2 W
-        tt = v.T @ np.linalg.solve(lch, (w / sd) * rv)
-        tt = tt / (1.0 / umu0 ** 2 - k2)
-        s = x @ tt
-        dd = linv(xd - mu * s / umu0)
-        zp = 0.5 * (s + dd)
-        zm = 0.5 * (s - dd)
+        ttv = v.T @ np.linalg.solve(lch, (w / sd) * rv)
+        ttv = ttv / (1.0 / umu0 ** 2 - k2)
+        svec = (sd / w) * (lch @ (v @ ttv))   # X tt, X = W^-1 D^1/2 L V
+        dd = linv(xd - mu * svec / umu0)
         att = math.exp(-tauc_top / umu0)
-        zp *= att
-        zm *= att
-        splus_src += zp - r @ zm - t @ (zp * e0)
-        sminus_src += zm * e0 - t @ zm - r @ (zp * e0)
+        zp = 0.5 * (svec + dd) * att
+        zm = 0.5 * (svec - dd) * att
+    db = b_bot - b_top
+    bsum = b_top + b_bot
     if b_top != 0.0 or b_bot != 0.0:
-        h = linv(mu)
-        qmh = qm @ h
-        one = np.ones(nn)
-        if taup > 0:
-            gfac = (b_bot - b_top) * (2.0 / taup) * qmh
-        else:
-            gfac = np.zeros(nn)
-        splus_src += b_top * (one - r @ one) - b_bot * (t @ one) + gfac
-        sminus_src += b_bot * (one - r @ one) - b_top * (t @ one) - gfac
+        b1 = db / taup if taup > 0 else 0.0
+        cvec = db + 2.0 * b1 * linv(mu)
+    else:
+        cvec = np.zeros(nn)
+    avec = zm - zp * e0
+    bvec = zm + zp * e0
+    pv = qtm @ (g * (cvec - avec))
+    qv = qtp @ (g * (bvec + bsum))
+    splus_src = g * (zp * (1 - e0) - db) + pv - qv
+    sminus_src = g * (-zm * (1 - e0) + db) - pv - qv
+    # back to the unscaled basis for the sweep in this model
+    r = rt * (1 / g)[:, None] * g[None, :]
+    t = tt_ * (1 / g)[:, None] * g[None, :]
+    splus_src = splus_src / g
+    sminus_src = sminus_src / g
     return dict(r=r, t=t, sp=splus_src, sm=sminus_src, taup=taup)
 
 

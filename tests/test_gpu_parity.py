@@ -1,0 +1,229 @@
+"""HIP path parity: libhdisort.so (through the C-ABI) vs the CPU oracle.
+
+Every test here runs the kernels on the GPU via pyharp_amd.Disort -> ctypes ->
+hd_solve and compares with the oracle on the same inputs.  Tolerance: the
+north-star bound max |dF|/F < 1e-6 (metric in tests/helpers.py).
+"""
+
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import TOL, case_bc, disotest, load_cases, rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _disort(nstr, nlyr, nwave, ncol, nmom=None, planck=False, wl=None, wu=None):
+    from pyharp_amd import Disort, DisortOptions
+    op = DisortOptions().flags("lamber,quiet,onlyfl" + (",planck" if planck else ""))
+    op.nwave(nwave).ncol(ncol)
+    if planck:
+        op.wave_lower(list(map(float, wl))).wave_upper(list(map(float, wu)))
+    op.ds().nlyr = nlyr
+    op.ds().nstr = nstr
+    op.ds().nmom = nstr if nmom is None else nmom
+    return Disort(op)
+
+
+def _run(d, prop, bc, temf=None, **kw):
+    dev = torch.device("cuda", 0)
+    p = torch.as_tensor(prop, dtype=torch.float64, device=dev)
+    b = {k: torch.as_tensor(v, dtype=torch.float64, device=dev) for k, v in bc.items()}
+    t = None if temf is None else torch.as_tensor(temf, dtype=torch.float64, device=dev)
+    return d.forward(p, b, t, **kw).cpu().numpy()
+
+
+def test_native_library_is_loaded():
+    from pyharp_amd import _lib
+    lib = _lib.load()
+    assert lib.hd_version() >= 100
+    assert torch.cuda.is_available()
+
+
+@pytest.mark.parametrize("case", ["1a", "1b", "1d"])
+def test_disotest1(case):
+    g = disotest()
+    c = g["cases"][case]
+    d = _disort(16, 1, 1, 1)
+    prop = np.zeros((1, 1, 1, 2 + 16))
+    prop[..., 0] = c["tau"]
+    prop[..., 1] = c["ssalb"]
+    bc = {"umu0": np.full((1, 1), 0.1), "fbeam": np.full((1, 1), math.pi / 0.1)}
+    f = _run(d, prop, bc)
+    flup_top, fdn_bot = f[0, 0, 1, 0], f[0, 0, 0, 1]
+    exp_up = c["flup"][0]
+    exp_dn = c["rfldir"][1] + c["rfldn"][1]
+    assert abs(flup_top - exp_up) <= 5e-6 * abs(exp_up) + 1e-6
+    assert abs(fdn_bot - exp_dn) <= 5e-6 * abs(exp_dn) + 1e-6
+
+
+@pytest.mark.parametrize("name", sorted(load_cases()))
+def test_golden_cases(name):
+    d = load_cases()[name]
+    prop = d["prop"]
+    nwave, ncol, nlyr, _ = prop.shape
+    planck = bool(d["planck"])
+    dis = _disort(int(d["nstr"]), nlyr, nwave, ncol, nmom=int(d["nmom"]), planck=planck,
+                  wl=d.get("wave_lower"), wu=d.get("wave_upper"))
+    f = _run(dis, prop, case_bc(d), d.get("temf"))
+    err = rel_err(f, d["flux"]).max()
+    assert err < TOL, f"{name}: max rel err {err:.3e}"
+
+
+def _random_batch(rng, nwave, ncol, nlyr, nstr, planck, beam=True, ssa_max=0.99, gmax=0.85):
+    nmom = nstr
+    prop = np.zeros((nwave, ncol, nlyr, 2 + nmom))
+    prop[..., 0] = 10.0 ** rng.uniform(-5, 0.7, (nwave, ncol, nlyr))
+    prop[..., 1] = rng.uniform(0, ssa_max, (nwave, ncol, nlyr))
+    g = rng.uniform(0, gmax, (nwave, ncol, nlyr))
+    for l in range(nmom):
+        prop[..., 2 + l] = g ** (l + 1)
+    bc = {"albedo": rng.uniform(0, 1, (nwave, ncol))}
+    if beam:
+        bc["fbeam"] = np.ones((nwave, ncol))
+        bc["umu0"] = rng.uniform(0.05, 1.0, (nwave, ncol))
+    kw = {}
+    if planck:
+        tl = np.linspace(300, 150, nlyr)[None, :] + rng.uniform(-5, 5, (ncol, nlyr))
+        from oracle.disort_np import layer2level
+        kw["temf"] = layer2level(tl)
+        bc["btemp"] = np.full((nwave, ncol), 295.0)
+        kw["wave_lower"] = np.sort(rng.uniform(10, 2500, nwave))
+        kw["wave_upper"] = kw["wave_lower"] + rng.uniform(1, 300, nwave)
+    return prop, bc, kw
+
+
+@pytest.mark.parametrize("nstr", [2, 4, 6, 8, 10, 12, 14, 16])
+@pytest.mark.parametrize("planck", [False, True])
+def test_vs_c_oracle(oracle_c, nstr, planck):
+    rng = np.random.default_rng(1000 + nstr + 100 * planck)
+    nwave, ncol, nlyr = 4, 8, 40
+    prop, bc, kw = _random_batch(rng, nwave, ncol, nlyr, nstr, planck)
+    ref = oracle_c.forward(prop, bc, kw.get("temf"), nstr=nstr, planck=planck,
+                           wave_lower=kw.get("wave_lower"), wave_upper=kw.get("wave_upper"))
+    d = _disort(nstr, nlyr, nwave, ncol, planck=planck, wl=kw.get("wave_lower"),
+                wu=kw.get("wave_upper"))
+    f = _run(d, prop, bc, kw.get("temf"))
+    err = rel_err(f, ref).max()
+    assert err < TOL, f"nstr={nstr} planck={planck}: max rel err {err:.3e}"
+
+
+def test_headline_config_subsample(oracle_c):
+    """C4 shape (nstr=16, nlyr=80, nmom=16): a 2048-solve slab vs the C oracle."""
+    rng = np.random.default_rng(20250217)
+    nwave, ncol, nlyr, nstr = 8, 256, 80, 16
+    prop, bc, _ = _random_batch(rng, nwave, ncol, nlyr, nstr, False)
+    d = _disort(nstr, nlyr, nwave, ncol)
+    f = _run(d, prop, bc)
+    idx = rng.choice(nwave * ncol, 128, replace=False)
+    ref = np.zeros_like(f)
+    for s in idx:
+        oracle_c.forward(prop, bc, nstr=nstr, first=int(s), count=1, out=ref)
+    fw = f.reshape(-1, nlyr + 1, 2)[idx]
+    rw = ref.reshape(-1, nlyr + 1, 2)[idx]
+    err = rel_err(fw, rw).max()
+    assert err < TOL, f"max rel err {err:.3e}"
+
+
+def test_chunking_invariance():
+    rng = np.random.default_rng(7)
+    prop, bc, _ = _random_batch(rng, 3, 37, 20, 8, False)
+    d = _disort(8, 20, 3, 37)
+    f1 = _run(d, prop, bc)
+    from pyharp_amd.disort import _context
+    ctx = _context(0)
+    ctx.set_chunk(17)
+    try:
+        f2 = _run(d, prop, bc)
+    finally:
+        ctx.set_chunk(0)
+    assert np.array_equal(f1, f2)
+
+
+def test_linearity_in_fbeam():
+    rng = np.random.default_rng(8)
+    prop, bc, _ = _random_batch(rng, 2, 16, 30, 16, False)
+    d = _disort(16, 30, 2, 16)
+    f1 = _run(d, prop, bc)
+    bc2 = dict(bc, fbeam=bc["fbeam"] * 3.0)
+    f3 = _run(d, prop, bc2)
+    assert rel_err(f3, 3.0 * f1).max() < 1e-12
+
+
+def test_conservative_energy_balance():
+    """omega=1 everywhere, albedo=1, beam only: net flux ~0 at every level
+    (exact but for DISORT's dither of ssalb=1 -> 1-4.7e-8)."""
+    rng = np.random.default_rng(9)
+    nwave, ncol, nlyr, nstr = 2, 8, 25, 16
+    prop, bc, _ = _random_batch(rng, nwave, ncol, nlyr, nstr, False)
+    prop[..., 1] = 1.0
+    bc["albedo"] = np.ones((nwave, ncol))
+    d = _disort(nstr, nlyr, nwave, ncol)
+    f = _run(d, prop, bc)
+    top_in = bc["fbeam"] * bc["umu0"]
+    net = (f[..., 0] - f[..., 1]) / top_in[..., None]
+    assert np.abs(net).max() < 1e-4
+    assert np.abs(f[:, :, -1, 0] / top_in - 1.0).max() < 1e-4
+
+
+def test_edge_cases(oracle_c):
+    nstr, nlyr = 8, 6
+    prop = np.zeros((1, 6, nlyr, 2 + nstr))
+    prop[..., 0] = 0.5
+    prop[0, 0, :, 0] = 0.0          # fully transparent column
+    prop[0, 1, :, 1] = 1.0          # conservative
+    prop[0, 2, 2, 0] = 0.0          # one empty layer
+    prop[0, 3, :, 1] = 0.5          # isotropic (no moments)
+    prop[0, 4, :, 0] = 50.0         # optically very thick
+    prop[0, 5, :, 1] = 0.9
+    for l in range(nstr):
+        prop[0, 5, :, 2 + l] = 0.8 ** (l + 1)
+    bc = {"fbeam": np.ones((1, 6)), "umu0": np.array([[1.0, 0.5, 0.3, 0.9, 0.7, 0.2]]),
+          "albedo": np.array([[0.0, 1.0, 0.5, 0.2, 0.3, 0.0]])}
+    ref = oracle_c.forward(prop, bc, nstr=nstr)
+    f = _run(_disort(nstr, nlyr, 1, 6), prop, bc)
+    assert rel_err(f, ref).max() < TOL
+    # transparent column: F_dn = mu0 F0 everywhere, F_up = albedo * mu0 F0 = 0
+    assert np.allclose(f[0, 0, :, 1], 1.0, rtol=1e-14)
+
+
+def test_empty_batch():
+    d = _disort(8, 5, 0, 3)
+    out = d.forward(torch.zeros((0, 3, 5, 10), dtype=torch.float64, device="cuda"), {})
+    assert tuple(out.shape) == (0, 3, 6, 2)
+
+
+def test_bad_input_raises():
+    d = _disort(8, 3, 1, 1)
+    prop = torch.zeros((1, 1, 3, 10), dtype=torch.float64, device="cuda")
+    prop[..., 0] = -1.0
+    with pytest.raises(RuntimeError, match="numerical failure"):
+        d.forward(prop, {})
+
+
+def test_status_buffer_async():
+    rng = np.random.default_rng(11)
+    prop, bc, _ = _random_batch(rng, 2, 4, 10, 8, False)
+    prop[1, 2, 3, 1] = 1.5  # invalid ssa -> bad input bit on that solve only
+    d = _disort(8, 10, 2, 4)
+    st = torch.zeros(8, dtype=torch.int32, device="cuda")
+    dev = torch.device("cuda", 0)
+    b = {k: torch.as_tensor(v, dtype=torch.float64, device=dev) for k, v in bc.items()}
+    d.forward(torch.as_tensor(prop, device=dev), b, status=st)
+    torch.cuda.synchronize()
+    s = st.cpu().numpy()
+    assert s[1 * 4 + 2] & 0x1
+    assert (np.delete(s, 6) & 0xF == 0).all()
+
+
+def test_cpu_tensors_round_trip(oracle_c):
+    rng = np.random.default_rng(12)
+    prop, bc, _ = _random_batch(rng, 2, 3, 8, 4, False)
+    d = _disort(4, 8, 2, 3)
+    out = d.forward(torch.as_tensor(prop), {k: torch.as_tensor(v) for k, v in bc.items()})
+    assert out.device.type == "cpu"
+    ref = oracle_c.forward(prop, bc, nstr=4)
+    assert rel_err(out.numpy(), ref).max() < TOL
