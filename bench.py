@@ -172,7 +172,8 @@ def main():
     from pyharp_amd.disort import _context
 
     ncol, nlyr, nstr, G = args.ncol, args.nlyr, args.nstr, args.ngpoint
-    gpoints = [g for g in range(G) if g % world == rank]
+    from pyharp_amd.spectral import allreduce_band_flux, band_flux, shard_gpoints
+    gpoints = shard_gpoints(G, world, rank)
     W = len(gpoints)
     wl_all, wu_all = wave_bounds(G)
     wl, wu = wl_all[gpoints], wu_all[gpoints]
@@ -190,11 +191,7 @@ def main():
 
     def step():
         disort.forward(prop, bc, temf, status=status, out=flux)
-        band = torch.einsum("g,gcld->cld", wts, flux)
-        if world > 1:
-            import torch.distributed as dist
-            dist.all_reduce(band)
-        return band
+        return allreduce_band_flux(band_flux(flux, wts))
 
     for _ in range(args.warmup):
         step()

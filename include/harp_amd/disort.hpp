@@ -1,0 +1,197 @@
+// harp_amd/disort.hpp -- libtorch drop-in for pydisort's `disort::Disort` module,
+// backed by the MI355X kernels of libhdisort.so (C-ABI: include/hdisort.h).
+//
+// pyharp builds its solver as
+//     rtsolver = torch::nn::AnyModule(disort::Disort(options.disort()));
+// (src/radiation/radiation_band.cpp:57-69) and calls
+//     rtsolver.forward(prop, &bc[, temf])      (radiation_band.cpp:123-128,
+//     examples/amars_sw.cpp:280, examples/amars_lw.cpp:80)
+// with the plugin contract of RTSolverImpl::forward (src/rtsolver/rtsolver.hpp:25-29).
+// Swapping `disort::Disort` for `harp_amd::Disort` keeps that code unchanged:
+//
+//     harp_amd::DisortOptions op;
+//     op.flags("lamber,quiet,onlyfl").nwave(nwave).ncol(ncol);
+//     op.ds().nlyr = nlyr; op.ds().nstr = 16; op.ds().nmom = 16;
+//     harp_amd::Disort disort(op);
+//     auto flux = disort->forward(prop, &bc);          // (nwave, ncol, nlyr+1, 2)
+//
+// Tensors may live on the CPU (staged through the GPU, result returned on the
+// CPU) or on a ROCm device (zero-copy, torch's current stream).  Errors are
+// raised with TORCH_CHECK, like the reference (radiation_band.cpp:25,50,71).
+#pragma once
+
+#include <ATen/hip/HIPContext.h>
+#include <torch/nn/cloneable.h>
+#include <torch/nn/module.h>
+#include <torch/nn/modules/container/any.h>
+#include <torch/torch.h>
+
+#include <map>
+#include <memory>
+#include <set>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../hdisort.h"
+
+namespace harp_amd {
+
+namespace index {
+constexpr int IEX = 0;  // optical thickness
+constexpr int ISS = 1;  // single-scattering albedo
+constexpr int IPM = 2;  // phase moments chi_1..chi_nmom
+constexpr int IUP = 0;  // upward flux
+constexpr int IDN = 1;  // downward flux (rfldir + rfldn)
+}  // namespace index
+
+#define HARP_AMD_ARG(T, name)                                         \
+ public:                                                             \
+  inline auto name(const T& v) -> decltype(*this) {                  \
+    this->name##_ = v;                                               \
+    return *this;                                                    \
+  }                                                                  \
+  inline const T& name() const noexcept { return this->name##_; }    \
+  inline T& name() noexcept { return this->name##_; }                \
+                                                                     \
+ private:                                                            \
+  T name##_
+
+struct DisortState {  // subset of cdisort's disort_state reachable via ds()
+  int nlyr = 1, nstr = 4, nmom = 4, nphi = 0, ntau = 0, numu = 0;
+};
+
+struct DisortOptions {
+  DisortOptions() = default;
+  DisortState& ds() { return ds_; }
+  const DisortState& ds() const { return ds_; }
+  HARP_AMD_ARG(std::string, header) = "";
+  HARP_AMD_ARG(std::string, flags) = "";
+  HARP_AMD_ARG(int, nwave) = 1;
+  HARP_AMD_ARG(int, ncol) = 1;
+  HARP_AMD_ARG(std::vector<double>, wave_lower) = {};
+  HARP_AMD_ARG(std::vector<double>, wave_upper) = {};
+  HARP_AMD_ARG(std::vector<double>, user_tau) = {};
+  HARP_AMD_ARG(std::vector<double>, user_mu) = {};
+  HARP_AMD_ARG(std::vector<double>, user_phi) = {};
+  HARP_AMD_ARG(int, device) = 0;
+
+ private:
+  DisortState ds_;
+};
+
+inline std::set<std::string> parse_flags(const std::string& s) {
+  std::set<std::string> out;
+  std::stringstream ss(s);
+  std::string tok;
+  while (std::getline(ss, tok, ',')) {
+    tok.erase(0, tok.find_first_not_of(" \t"));
+    tok.erase(tok.find_last_not_of(" \t") + 1);
+    if (!tok.empty()) out.insert(tok);
+  }
+  return out;
+}
+
+class DisortImpl : public torch::nn::Cloneable<DisortImpl> {
+ public:
+  DisortOptions options;
+
+  DisortImpl() = default;
+  explicit DisortImpl(DisortOptions const& op) : options(op) { reset(); }
+
+  void reset() override {
+    static const std::set<std::string> known = {
+        "lamber", "quiet", "onlyfl", "planck", "usrtau", "usrang", "intensity_correction",
+        "old_intensity_correction", "print-input", "print-fluxes", "print-intensity",
+        "print-transmissivity", "print-phase-function", "deltam", "lyrcut", "ibcnd"};
+    auto flags = parse_flags(options.flags());
+    for (auto const& f : flags) TORCH_CHECK(known.count(f), "Disort: unknown flag ", f);
+    TORCH_CHECK(flags.count("lamber"), "Disort: only Lambertian lower boundaries are supported");
+    auto const& ds = options.ds();
+    TORCH_CHECK(ds.nstr >= 2 && ds.nstr % 2 == 0 && ds.nstr <= 16,
+                "Disort: nstr must be even and in [2, 16]");
+    TORCH_CHECK(ds.nlyr >= 1, "Disort: nlyr must be >= 1");
+    planck_ = flags.count("planck") > 0;
+    if (planck_)
+      TORCH_CHECK((int)options.wave_lower().size() == options.nwave() &&
+                      (int)options.wave_upper().size() == options.nwave(),
+                  "Disort: planck needs wave_lower/wave_upper of size nwave");
+  }
+
+  DisortState& ds() { return options.ds(); }
+
+  //! flux (nwave, ncol, nlyr+1, 2); level 0 = surface; [..,0] up, [..,1] down
+  torch::Tensor forward(torch::Tensor prop, std::map<std::string, torch::Tensor>* bc,
+                        torch::optional<torch::Tensor> temf = torch::nullopt) {
+    TORCH_CHECK(prop.dim() == 4, "Disort.forward: prop must be (nwave, ncol, nlyr, nprop)");
+    const int nwave = prop.size(0), ncol = prop.size(1), nlyr = prop.size(2),
+              nprop = prop.size(3);
+    TORCH_CHECK(nlyr == options.ds().nlyr, "Disort.forward: prop has ", nlyr,
+                " layers, ds().nlyr = ", options.ds().nlyr);
+    TORCH_CHECK(!planck_ || temf.has_value(), "Disort.forward: planck flag set but temf missing");
+    auto in_dev = prop.device();
+    torch::Device dev = in_dev.is_cuda() ? in_dev : torch::Device(torch::kCUDA, options.device());
+    auto f64 = torch::TensorOptions().dtype(torch::kFloat64).device(dev);
+    auto to_dev = [&](torch::Tensor t) { return t.to(f64).contiguous(); };
+
+    auto p = to_dev(prop);
+    static const char* keys[] = {"fbeam", "umu0", "albedo", "btemp", "ttemp", "temis", "fisot"};
+    std::map<std::string, torch::Tensor> b;
+    if (bc) {
+      for (auto const& [k, v] : *bc) {
+        bool ok = k == "phi0";
+        for (auto key : keys) ok = ok || k == key;
+        TORCH_CHECK(ok, "Disort.forward: unknown boundary condition '", k, "'");
+        if (k == "phi0") continue;
+        auto t = to_dev(v.expand({nwave, ncol}));
+        b[k] = t;
+      }
+    }
+    torch::Tensor tf, wl, wu;
+    if (planck_) {
+      tf = to_dev(*temf);
+      TORCH_CHECK(tf.size(0) == ncol && tf.size(1) == nlyr + 1,
+                  "Disort.forward: temf must be (ncol, nlyr+1)");
+      wl = torch::tensor(options.wave_lower(), f64);
+      wu = torch::tensor(options.wave_upper(), f64);
+    }
+    auto flux = torch::empty({nwave, ncol, nlyr + 1, 2}, f64);
+
+    auto ptr = [](const torch::Tensor& t) -> const double* {
+      return t.defined() ? t.data_ptr<double>() : nullptr;
+    };
+    auto bp = [&](const char* k) -> const double* {
+      auto it = b.find(k);
+      return it == b.end() ? nullptr : it->second.data_ptr<double>();
+    };
+    hd_config cfg{options.ds().nstr, options.ds().nmom, nlyr, nprop,
+                  HD_FLAG_LAMBER | HD_FLAG_ONLYFL | (planck_ ? HD_FLAG_PLANCK : 0u)};
+    hd_inputs in{nwave,       ncol,        ptr(p),        bp("fbeam"), bp("umu0"),
+                 bp("albedo"), bp("btemp"), bp("ttemp"),  bp("temis"), bp("fisot"),
+                 ptr(tf),     ptr(wl),     ptr(wu)};
+    auto stream = at::hip::getCurrentHIPStream(dev.index()).stream();
+    int rc = hd_solve(context(dev.index()), &cfg, &in, flux.data_ptr<double>(), nullptr,
+                      reinterpret_cast<void*>(stream));
+    TORCH_CHECK(rc == HD_OK, "DisortWrapper::Run failed: ", hd_last_error(context(dev.index())));
+    return in_dev.is_cuda() ? flux : flux.to(in_dev);
+  }
+
+ private:
+  bool planck_ = false;
+
+  static hd_context* context(int device) {
+    static std::map<int, std::unique_ptr<hd_context, int (*)(hd_context*)>> ctxs;
+    auto it = ctxs.find(device);
+    if (it != ctxs.end()) return it->second.get();
+    hd_context* c = nullptr;
+    int rc = hd_context_create(&c, device);
+    TORCH_CHECK(rc == HD_OK, "Disort: ", hd_last_error(nullptr));
+    ctxs.emplace(device, std::unique_ptr<hd_context, int (*)(hd_context*)>(c, hd_context_destroy));
+    return c;
+  }
+};
+TORCH_MODULE(Disort);
+
+#undef HARP_AMD_ARG
+
+}  // namespace harp_amd

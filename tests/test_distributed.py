@@ -1,0 +1,70 @@
+"""The N>1 path on CPU: spectral sharding + one all-reduce of the band flux.
+
+Two gloo ranks each solve their own g-points (with the CPU oracle standing in
+for the device solve -- test infrastructure only) and complete the band flux
+with pyharp_amd.spectral.allreduce_band_flux; the result must equal the
+single-process band sum.
+"""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _problem():
+    rng = np.random.default_rng(3)
+    G, C, L, nstr = 6, 3, 5, 4
+    prop = np.zeros((G, C, L, 2 + nstr))
+    prop[..., 0] = 10 ** rng.uniform(-2, 0.5, (G, C, L))
+    prop[..., 1] = rng.uniform(0, 0.9, (G, C, L))
+    bc = {"fbeam": np.ones((G, C)), "umu0": rng.uniform(0.2, 1, (G, C)),
+          "albedo": rng.uniform(0, 1, (G, C))}
+    w = rng.uniform(0.1, 1.0, G)
+    return prop, bc, w / w.sum(), nstr
+
+
+def _worker(rank, world, port, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle_c
+    from pyharp_amd.spectral import allreduce_band_flux, band_flux, shard_gpoints
+    prop, bc, w, nstr = _problem()
+    mine = shard_gpoints(prop.shape[0], world, rank)
+    flux = oracle_c.forward(prop[mine], {k: v[mine] for k, v in bc.items()}, nstr=nstr)
+    part = band_flux(torch.as_tensor(flux), torch.as_tensor(w[mine]))
+    allreduce_band_flux(part)
+    if rank == 0:
+        np.save(out_path, part.numpy())
+    dist.destroy_process_group()
+
+
+def test_shard_gpoints_partition():
+    from pyharp_amd.spectral import shard_gpoints
+    for world in (1, 2, 3, 8):
+        allg = sorted(g for r in range(world) for g in shard_gpoints(64, world, r))
+        assert allg == list(range(64))
+    with pytest.raises(ValueError):
+        shard_gpoints(8, 2, 2)
+
+
+def test_two_rank_band_flux(tmp_path, oracle_c):
+    out = str(tmp_path / "band.npy")
+    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    prop, bc, w, nstr = _problem()
+    ref = np.einsum("g,gcld->cld", w, oracle_c.forward(prop, bc, nstr=nstr))
+    got = np.load(out)
+    np.testing.assert_allclose(got, ref, rtol=1e-13, atol=1e-16)

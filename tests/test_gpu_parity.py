@@ -227,3 +227,30 @@ def test_cpu_tensors_round_trip(oracle_c):
     assert out.device.type == "cpu"
     ref = oracle_c.forward(prop, bc, nstr=4)
     assert rel_err(out.numpy(), ref).max() < TOL
+
+
+def test_cpp_dropin(oracle_c):
+    """C++ libtorch module harp_amd::Disort (include/harp_amd/disort.hpp) used with
+    the reference's SW call pattern; compiled by tests/cpp/build.sh."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "tests", "cpp", "disort_dropin")
+    if not os.path.exists(exe):
+        subprocess.run([os.path.join(root, "tests", "cpp", "build.sh")], check=True)
+    out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout
+    nwave, ncol, nlyr, nstr = 6, 2, 12, 8
+    got = np.zeros((nwave, ncol, nlyr + 1, 2))
+    for line in out.strip().splitlines():
+        w, c, l, up, dn = line.split()
+        got[int(w), int(c), int(l)] = (float(up), float(dn))
+    prop = np.zeros((nwave, ncol, nlyr, 2))
+    for w in range(nwave):
+        for c in range(ncol):
+            for l in range(nlyr):
+                prop[w, c, l, 0] = 0.01 * (1 + w) * (1 + l % 3) + 0.05 * c
+                prop[w, c, l, 1] = 0.3 + 0.05 * w + 0.02 * (l % 4)
+    bc = {"fbeam": np.ones((nwave, ncol)), "umu0": np.ones((nwave, ncol)),
+          "albedo": np.ones((nwave, ncol))}
+    ref = oracle_c.forward(prop, bc, nstr=nstr)
+    assert rel_err(got, ref).max() < TOL

@@ -1,0 +1,137 @@
+"""The C-ABI library and the host-side module, without a GPU.
+
+Checks that libhdisort.so builds/loads and exports every symbol declared in
+include/hdisort.h, the host helpers, option validation and the loud failure
+when no HIP device is present (no CPU fallback).
+"""
+
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_functions():
+    with open(os.path.join(ROOT, "include", "hdisort.h")) as f:
+        src = f.read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(hd_[a-z_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from pyharp_amd import _build, _lib
+    _build.build()
+    return _lib.load()
+
+
+def test_exports_every_declared_symbol(lib):
+    from pyharp_amd import _lib
+    names = _declared_functions()
+    assert "hd_solve" in names and len(names) >= 10
+    for name in names:
+        assert hasattr(lib, name), name
+    assert set(names) == set(_lib.EXPORTED)
+
+
+def test_version(lib):
+    assert lib.hd_version() == 100
+
+
+@pytest.mark.parametrize("nstr", [2, 4, 8, 16])
+def test_quadrature_matches_gauss_legendre(nstr):
+    from pyharp_amd import _lib
+    mu, w = _lib.quadrature(nstr)
+    x, wx = np.polynomial.legendre.leggauss(nstr // 2)
+    np.testing.assert_allclose(mu, 0.5 * (x + 1), rtol=0, atol=1e-15)
+    np.testing.assert_allclose(w, 0.5 * wx, rtol=0, atol=1e-15)
+
+
+def test_quadrature_rejects_odd(lib):
+    mu = (ctypes.c_double * 4)()
+    assert lib.hd_quadrature(5, mu, mu) == 1
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="CPU-only behaviour")
+def test_no_device_fails_loudly(lib):
+    h = ctypes.c_void_p()
+    rc = lib.hd_context_create(ctypes.byref(h), 0)
+    assert rc != 0
+    from pyharp_amd import Disort, DisortOptions
+    op = DisortOptions().flags("lamber,onlyfl").nwave(1).ncol(1)
+    op.ds().nlyr, op.ds().nstr, op.ds().nmom = 2, 4, 4
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        Disort(op).forward(torch.zeros((1, 1, 2, 6), dtype=torch.float64), {})
+
+
+def test_null_context_rejected(lib):
+    from pyharp_amd import _lib
+    cfg = _lib.HdConfig(nstr=4, nmom=4, nlyr=2, nprop=6, flags=1)
+    inp = _lib.HdInputs(nwave=1, ncol=1)
+    assert lib.hd_solve(None, ctypes.byref(cfg), ctypes.byref(inp), None, None, None) == 1
+
+
+def test_options_validation():
+    from pyharp_amd import Disort, DisortOptions
+    op = DisortOptions().flags("lamber,onlyfl,bogus")
+    with pytest.raises(RuntimeError, match="unknown flags"):
+        Disort(op)
+    op = DisortOptions().flags("lamber")
+    op.ds().nstr = 5
+    with pytest.raises(RuntimeError, match="nstr"):
+        Disort(op)
+    op = DisortOptions().flags("onlyfl")
+    with pytest.raises(RuntimeError, match="Lambertian"):
+        Disort(op)
+    op = DisortOptions().flags("lamber,planck").nwave(2)
+    with pytest.raises(RuntimeError, match="wave_lower"):
+        Disort(op)
+
+
+def test_option_accessors_follow_add_arg_idiom():
+    from pyharp_amd import DisortOptions
+    op = DisortOptions()
+    assert op.nwave(7) is op and op.nwave() == 7
+    op.ds().nlyr = 40
+    assert op.ds().nlyr == 40
+
+
+def test_rtsolver_base_raises():
+    from pyharp_amd import RTSolver
+    with pytest.raises(RuntimeError, match="not implemented"):
+        RTSolver().forward(None, {})
+
+
+def test_forward_shape_errors():
+    from pyharp_amd import Disort, DisortOptions
+    op = DisortOptions().flags("lamber,onlyfl").nwave(1).ncol(1)
+    op.ds().nlyr, op.ds().nstr = 3, 4
+    d = Disort(op)
+    with pytest.raises(RuntimeError, match="layers"):
+        d.forward(torch.zeros((1, 1, 2, 6), dtype=torch.float64), {})
+    with pytest.raises(RuntimeError, match="unknown boundary"):
+        d.forward(torch.zeros((1, 1, 3, 6), dtype=torch.float64), {"fbam": torch.ones(1, 1)})
+
+
+def test_layer2level_torch_matches_reference_run():
+    from pyharp_amd import layer2level
+    out = layer2level(torch.tensor([[300.0, 280.0, 260.0, 250.0, 240.0]], dtype=torch.float64))
+    np.testing.assert_allclose(out[0].numpy(),
+                               [310.0, 290.0, 269.1666666667, 254.1666666667, 245.0, 240.0],
+                               rtol=1e-10)
+
+
+def test_product_never_imports_oracle():
+    pkg = os.path.join(ROOT, "pyharp_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for fn in files:
+            if fn.endswith((".py", ".cpp", ".hip", ".hpp", ".h")):
+                with open(os.path.join(dirpath, fn)) as f:
+                    src = f.read()
+                assert not re.search(r"^\s*(from|import)\s+oracle", src, re.M), fn
+                assert "hdoracle" not in src, fn
