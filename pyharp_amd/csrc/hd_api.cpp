@@ -324,6 +324,16 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
     double* layer_ops = ctx->scratch;
     double* bsub = layer_ops + ne1 * nlyr * (size_t)nsc;
     double* planckv = planck ? bsub + ne2 * nlyr * (size_t)nsc : nullptr;
+    double* taucv = bsub + ne2 * nlyr * (size_t)nsc + (planck ? (size_t)(nlyr + 3) * nsc : 0);
+    hd::TaucArgs ta{};
+    ta.prop = in->prop;
+    ta.out = taucv;
+    ta.s0 = s0;
+    ta.nsc = nsc;
+    ta.nlyr = nlyr;
+    ta.nprop = cfg->nprop;
+    ta.use_f = nm >= cfg->nstr;
+    ta.f_slot = 1 + cfg->nstr;
     hd::PlanckArgs pa{};
     pa.temf = in->temf;
     pa.btemp = in->btemp;
@@ -338,6 +348,7 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
     pa.nlyr = nlyr;
     hd::LayerArgs la{};
     la.prop = in->prop;
+    la.tauc = taucv;
     la.fbeam = in->fbeam;
     la.umu0 = in->umu0;
     la.planckv = planckv;
@@ -382,7 +393,9 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
       ev = &ctx->pool[ctx->pool_used];
       ctx->pool_used += 3;
     }
-    hipError_t e = hd::launch_solve_chunk_nn(nn, planck ? &pa : nullptr, la, sa, stream, ev);
+    const bool beam = in->fbeam != nullptr;
+    hipError_t e = hd::launch_solve_chunk_nn(nn, planck ? &pa : nullptr, beam ? &ta : nullptr, la,
+                                             sa, stream, ev);
     if (e != hipSuccess) return fail(ctx, HD_EHIP, "hd_solve: launch failed: %s", hipGetErrorString(e));
   }
   if (sync) {

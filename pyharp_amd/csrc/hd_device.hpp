@@ -34,8 +34,31 @@ struct Quad {
   double w[NN];           // weights, sum = 1
   double sd[NN];          // sqrt(w/mu)
   double g[NN];           // sqrt(w*mu)  (flux-weighted basis scale)
+  double rmu[NN];         // 1/mu
+  double rg[NN];          // 1/g = sd/w   (note w/sd = g)
   double pt[2 * NN][NN];  // P_l(mu_i), l < nstr
 };
+
+// ----------------------------------------------------------------------------
+// reciprocal / reciprocal square root: hardware estimate + 2 Newton steps
+// (no IEEE division sequence; inputs are finite and nonzero where used)
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ double rcp_nr(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
+
+__device__ __forceinline__ double rsq_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x;
+  double e = fma(-h * y, y, 0.5);
+  y = fma(y, e, y);
+  e = fma(-h * y, y, 0.5);
+  return fma(y, e, y);
+}
 
 // symmetric access to the upper triangle (i, j compile-time after unrolling)
 #define HD_SYM(a, i, j) a[((i) < (j) ? (i) : (j))][((i) < (j) ? (j) : (i))]
@@ -109,129 +132,125 @@ __device__ inline double plkavg(double wlo, double whi, double t) {
 // small dense kernels on register arrays
 // ----------------------------------------------------------------------------
 
-// Cholesky of the SPD matrix in the upper triangle of a -> lower factor l.
-// returns false on breakdown.
-template <int NN>
-__device__ __forceinline__ bool chol_lower(const double (&a)[NN][NN], double (&l)[NN][NN]) {
-  bool ok = true;
-#pragma unroll
-  for (int j = 0; j < NN; ++j) {
-    double s = HD_SYM(a, j, j);
-#pragma unroll
-    for (int k = 0; k < j; ++k) s -= l[j][k] * l[j][k];
-    ok = ok && (s > 0.0);
-    const double d = sqrt(s > 0.0 ? s : 1e-300);
-    const double rd = 1.0 / d;
-    l[j][j] = d;
-#pragma unroll
-    for (int i = j + 1; i < NN; ++i) {
-      double t = HD_SYM(a, i, j);
-#pragma unroll
-      for (int k = 0; k < j; ++k) t -= l[i][k] * l[j][k];
-      l[i][j] = t * rd;
-    }
-  }
-  return ok;
-}
-
 // In-place Cholesky: reads the SPD matrix from the upper triangle of a and
 // writes the lower factor (diagonal included) into the lower triangle of the
-// same array (the strict upper triangle keeps the input).
+// same array (the strict upper triangle keeps the input); rd = 1/diag(L).
 template <int NN>
-__device__ __forceinline__ bool chol_inplace(double (&a)[NN][NN]) {
+__device__ __forceinline__ bool chol_inplace(double (&a)[NN][NN], double (&rd)[NN]) {
   bool ok = true;
 #pragma unroll
   for (int j = 0; j < NN; ++j) {
     double s = a[j][j];
 #pragma unroll
-    for (int k = 0; k < j; ++k) s -= a[j][k] * a[j][k];
+    for (int k = 0; k < j; ++k) s = fma(-a[j][k], a[j][k], s);
     ok = ok && (s > 0.0);
-    const double d = sqrt(s > 0.0 ? s : 1e-300);
-    const double rd = 1.0 / d;
-    a[j][j] = d;
+    s = s > 1e-300 ? s : 1e-300;
+    const double r = rsq_nr(s);
+    a[j][j] = s * r;
+    rd[j] = r;
 #pragma unroll
     for (int i = j + 1; i < NN; ++i) {
       double t = a[j][i];
 #pragma unroll
-      for (int k = 0; k < j; ++k) t -= a[i][k] * a[j][k];
-      a[i][j] = t * rd;
+      for (int k = 0; k < j; ++k) t = fma(-a[i][k], a[j][k], t);
+      a[i][j] = t * r;
     }
   }
   return ok;
 }
 
-// x <- L^-1 x (forward substitution, L lower)
+// x <- L^-1 x (forward substitution, L lower, rd = 1/diag(L))
 template <int NN>
-__device__ __forceinline__ void lower_solve(const double (&l)[NN][NN], double (&x)[NN]) {
+__device__ __forceinline__ void lower_solve(const double (&l)[NN][NN], const double (&rd)[NN],
+                                            double (&x)[NN]) {
 #pragma unroll
   for (int i = 0; i < NN; ++i) {
     double s = x[i];
 #pragma unroll
-    for (int k = 0; k < i; ++k) s -= l[i][k] * x[k];
-    x[i] = s / l[i][i];
+    for (int k = 0; k < i; ++k) s = fma(-l[i][k], x[k], s);
+    x[i] = s * rd[i];
   }
 }
 
 // x <- L^-T x (back substitution with the transpose of lower L)
 template <int NN>
-__device__ __forceinline__ void lower_t_solve(const double (&l)[NN][NN], double (&x)[NN]) {
+__device__ __forceinline__ void lower_t_solve(const double (&l)[NN][NN], const double (&rd)[NN],
+                                              double (&x)[NN]) {
 #pragma unroll
   for (int i = NN - 1; i >= 0; --i) {
     double s = x[i];
 #pragma unroll
-    for (int k = i + 1; k < NN; ++k) s -= l[k][i] * x[k];
-    x[i] = s / l[i][i];
+    for (int k = i + 1; k < NN; ++k) s = fma(-l[k][i], x[k], s);
+    x[i] = s * rd[i];
   }
 }
 
-// One Jacobi rotation on the symmetric matrix a (upper triangle) zeroing
-// a[p][q]; accumulates the rotation into the columns of v.
-template <int NN, int P, int Q>
-__device__ __forceinline__ void jacobi_rot(double (&a)[NN][NN], double (&v)[NN][NN], bool on) {
-  const double apq = a[P][Q];
-  const double app = a[P][P];
-  const double aqq = a[Q][Q];
-  const double d = aqq - app;
-  const double den = fabs(d) + sqrt(d * d + 4.0 * apq * apq);
-  double t = (den > 0.0 && on) ? 2.0 * apq / den : 0.0;  // converged lanes: exact no-op
-  t = d < 0.0 ? -t : t;
-  const double c = 1.0 / sqrt(1.0 + t * t);
-  const double s = t * c;
-  a[P][P] = app - t * apq;
-  a[Q][Q] = aqq + t * apq;
-  a[P][Q] = on ? 0.0 : apq;
-#pragma unroll
-  for (int r = 0; r < NN; ++r) {
-    if (r == P || r == Q) continue;
-    const double arp = HD_SYM(a, r, P);
-    const double arq = HD_SYM(a, r, Q);
-    HD_SYM(a, r, P) = c * arp - s * arq;
-    HD_SYM(a, r, Q) = s * arp + c * arq;
-  }
-#pragma unroll
-  for (int k = 0; k < NN; ++k) {
-    const double vkp = v[k][P];
-    const double vkq = v[k][Q];
-    v[k][P] = c * vkp - s * vkq;
-    v[k][Q] = s * vkp + c * vkq;
-  }
+// ----------------------------------------------------------------------------
+// Jacobi eigensolver, parallel (round-robin tournament) ordering: a sweep is
+// P-1 rounds of P/2 disjoint rotations (P = NN rounded up to even).  The
+// rotations of a round are independent, so their parameters (sqrt, rcp, rsq)
+// and updates interleave -- ILP for one wave per SIMD.
+// ----------------------------------------------------------------------------
+__host__ __device__ constexpr int tour_a(int P, int r, int k) {
+  return k == 0 ? P - 1 : (r + k) % (P - 1);
+}
+__host__ __device__ constexpr int tour_b(int P, int r, int k) {
+  return k == 0 ? r : (r - k + (P - 1)) % (P - 1);
 }
 
-template <int NN, int P, int Q>
-struct JacobiSweep {
-  __device__ __forceinline__ static void run(double (&a)[NN][NN], double (&v)[NN][NN], bool on) {
-    jacobi_rot<NN, P, Q>(a, v, on);
-    if constexpr (Q + 1 < NN) {
-      JacobiSweep<NN, P, Q + 1>::run(a, v, on);
-    } else if constexpr (P + 2 < NN) {
-      JacobiSweep<NN, P + 1, P + 2>::run(a, v, on);
+template <int NN>
+__device__ __forceinline__ void jacobi_round(int r, double (&a)[NN][NN], double (&v)[NN][NN],
+                                             bool on) {
+  constexpr int P = NN + (NN & 1);
+  constexpr int H = P / 2;
+  double cc[H], ss[H], tt[H];
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    const int x = tour_a(P, r, k), y = tour_b(P, r, k);
+    const int p = x < y ? x : y, q = x < y ? y : x;
+    if (q >= NN) continue;
+    const double apq = a[p][q];
+    const double d = a[q][q] - a[p][p];
+    const double den = fabs(d) + sqrt(fma(d, d, 4.0 * apq * apq));
+    double t = (den > 0.0 && on) ? 2.0 * apq * rcp_nr(den > 0.0 ? den : 1.0) : 0.0;
+    t = d < 0.0 ? -t : t;
+    const double c = rsq_nr(fma(t, t, 1.0));
+    cc[k] = c;
+    ss[k] = t * c;
+    tt[k] = t;
+  }
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    const int x = tour_a(P, r, k), y = tour_b(P, r, k);
+    const int p = x < y ? x : y, q = x < y ? y : x;
+    if (q >= NN) continue;
+    const double c = cc[k], s = ss[k], t = tt[k];
+    const double apq = a[p][q];
+    a[p][p] = fma(-t, apq, a[p][p]);
+    a[q][q] = fma(t, apq, a[q][q]);
+    a[p][q] = on ? 0.0 : apq;
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      if (i == p || i == q) continue;
+      const double aip = HD_SYM(a, i, p);
+      const double aiq = HD_SYM(a, i, q);
+      HD_SYM(a, i, p) = fma(c, aip, -s * aiq);
+      HD_SYM(a, i, q) = fma(s, aip, c * aiq);
+    }
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      const double vip = v[i][p];
+      const double viq = v[i][q];
+      v[i][p] = fma(c, vip, -s * viq);
+      v[i][q] = fma(s, vip, c * viq);
     }
   }
-};
+}
 
-// Cyclic Jacobi: a (upper triangle, symmetric) -> eigenvalues on the diagonal,
-// eigenvectors in the columns of v.  Sweeps until every lane of the wave has
-// converged (wave-uniform exit) or max_sweeps.
+// a (upper triangle, symmetric) -> eigenvalues on the diagonal, eigenvectors
+// in the columns of v.  A lane that has converged stops rotating (exact
+// no-ops), so its result does not depend on which solves share its wave; the
+// loop exits when every lane of the wave has converged or after max_sweeps.
 template <int NN>
 __device__ __forceinline__ void jacobi_eig(double (&a)[NN][NN], double (&v)[NN][NN],
                                            int max_sweeps) {
@@ -240,19 +259,19 @@ __device__ __forceinline__ void jacobi_eig(double (&a)[NN][NN], double (&v)[NN][
 #pragma unroll
     for (int j = 0; j < NN; ++j) v[i][j] = (i == j) ? 1.0 : 0.0;
   if constexpr (NN > 1) {
+    constexpr int P = NN + (NN & 1);
     for (int sweep = 0; sweep < max_sweeps; ++sweep) {
       double off = 0.0, dia = 0.0;
 #pragma unroll
       for (int i = 0; i < NN; ++i) {
-        dia += a[i][i] * a[i][i];
+        dia = fma(a[i][i], a[i][i], dia);
 #pragma unroll
-        for (int j = i + 1; j < NN; ++j) off += a[i][j] * a[i][j];
+        for (int j = i + 1; j < NN; ++j) off = fma(a[i][j], a[i][j], off);
       }
-      // per-lane convergence: a converged lane stops rotating, so its result
-      // does not depend on which other solves share the wave
       const bool done = !(off > 1.0e-34 * dia);
       if (__all(done)) break;
-      JacobiSweep<NN, 0, 1>::run(a, v, !done);
+#pragma unroll
+      for (int r = 0; r < P - 1; ++r) jacobi_round<NN>(r, a, v, !done);
     }
   }
 }

@@ -50,6 +50,10 @@ __device__ __forceinline__ const Quad<NN>& quad() {
 
 constexpr int kLayerBlock = 256;
 
+// phase boundary: keeps the scheduler from hoisting the next phase's loads
+// (and their registers) above the current phase
+#define HD_PHASE() __builtin_amdgcn_sched_barrier(0)
+
 // ============================================================================
 // K0: Planck radiance per (solve, level)
 // ============================================================================
@@ -72,6 +76,26 @@ __global__ __launch_bounds__(256) void hd_planck_kernel(PlanckArgs A) {
     b = te != 0.0 ? te * plkavg(A.wlo[w], A.whi[w], A.ttemp ? A.ttemp[s] : 0.0) : 0.0;
   }
   A.out[(size_t)lev * A.nsc + sl] = b;
+}
+
+// ============================================================================
+// K0b: cumulative delta-M-scaled optical depth above every layer (beam only)
+// ============================================================================
+__global__ __launch_bounds__(256) void hd_tauc_kernel(TaucArgs A) {
+  const long sl = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (sl >= A.nsc) return;
+  const long s = A.s0 + sl;
+  const int L = A.nlyr, np = A.nprop;
+  const double* p = A.prop + (size_t)s * L * np;
+  double tauc = 0.0;
+  for (int lc = 0; lc < L; ++lc) {  // solver order: top (harp layer L-1) first
+    const double* q = p + (size_t)(L - 1 - lc) * np;
+    double a = np > 1 ? q[1] : 0.0;
+    if (a == 1.0) a = 1.0 - kDither;
+    const double f = A.use_f ? q[A.f_slot] : 0.0;
+    A.out[(size_t)lc * A.nsc + sl] = tauc;
+    tauc += (1.0 - a * f) * q[0];
+  }
 }
 
 // ============================================================================
@@ -106,99 +130,101 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
   const double taup = (1.0 - ssa * f) * tau;
   const double om = ssa * (1.0 - f) / (1.0 - ssa * f);
   const double rf = om / (1.0 - f);
-  double gl[N];
-#pragma unroll
-  for (int l = 0; l < N; ++l) {
-    const double chi = l == 0 ? 1.0 : (l <= nm ? q[1 + l] : 0.0);
-    gl[l] = (2 * l + 1) * (chi - f) * rf;
-  }
 
   const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
   const double fb = A.fbeam ? A.fbeam[s] : 0.0;
   const bool beam = fb > 0.0 && mu0 > 0.0;
   if (beam && mu0 > 1.0) st |= kStBadInput;
   const double rmu0 = beam ? 1.0 / mu0 : 0.0;
+  const double mub = beam ? mu0 : 0.0;
 
-  // ---- beam source vectors xs, xd (even/odd Legendre parts) ----
-  double xs[NN], xd[NN];
-  if (beam) {
-    double pl0[N];
-    pl0[0] = 1.0;
-    if (N > 1) pl0[1] = mu0;
-#pragma unroll
-    for (int l = 2; l < N; ++l)
-      pl0[l] = ((2 * l - 1) * mu0 * pl0[l - 1] - (l - 1) * pl0[l - 2]) * (1.0 / l);
-    const double fb2 = fb * (0.5 / kPi);
-#pragma unroll
-    for (int i = 0; i < NN; ++i) {
-      double se = 0.0, so = 0.0;
-#pragma unroll
-      for (int l = 0; l < N; ++l) {
-        const double t = gl[l] * pl0[l] * Qc.pt[l][i];
-        if (l % 2 == 0) se += t; else so += t;
-      }
-      xs[i] = fb2 * se;
-      xd[i] = -fb2 * so;
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < NN; ++i) xs[i] = xd[i] = 0.0;
-  }
-
-  // ---- phase matrix even/odd parts -> -A- (lch), -A+ (ap), upper triangles ----
-  double lch[NN][NN], ap[NN][NN];
+  // ---- phase matrix even/odd parts (-A+ in ap, -A- in lch, upper) and the
+  //      beam source vectors; one even/odd Legendre pair per iteration so the
+  //      constant tables stream through a few scalar registers ----
+  double lch[NN][NN], ap[NN][NN], xs[NN], xd[NN];
 #pragma unroll
   for (int i = 0; i < NN; ++i) {
+    xs[i] = xd[i] = 0.0;
 #pragma unroll
-    for (int j = i; j < NN; ++j) {
-      double se = 0.0, so = 0.0;
+    for (int j = i; j < NN; ++j) lch[i][j] = ap[i][j] = 0.0;
+  }
+  {
+    double pprev = 0.0, pcur = 1.0;  // P_{l-1}(mu0), P_l(mu0) for the beam
+#pragma nounroll
+    for (int l2 = 0; l2 < NN; ++l2) {
+      const int le = 2 * l2, lo = le + 1;
+      const double che = le == 0 ? 1.0 : (le <= nm ? q[1 + le] : 0.0);
+      const double cho = lo <= nm ? q[1 + lo] : 0.0;
+      const double ge = (2 * le + 1) * (che - f) * rf;
+      const double go = (2 * lo + 1) * (cho - f) * rf;
+      const double pe0 = pcur;  // P_le(mu0)
+      const double po0 = ((2 * lo - 1) * mub * pcur - (lo - 1) * pprev) / lo;
+      pprev = po0;
+      pcur = ((2 * lo + 1) * mub * po0 - lo * pe0) / (lo + 1);
+      double ue[NN], uo[NN];
 #pragma unroll
-      for (int l = 0; l < N; ++l) {
-        const double t = gl[l] * Qc.pt[l][i] * Qc.pt[l][j];
-        if (l % 2 == 0) se += t; else so += t;
+      for (int i = 0; i < NN; ++i) {
+        ue[i] = ge * Qc.pt[le][i];
+        uo[i] = go * Qc.pt[lo][i];
+        xs[i] = fma(ue[i], pe0, xs[i]);
+        xd[i] = fma(uo[i], po0, xd[i]);
       }
-      const double diag = (i == j) ? 1.0 / Qc.mu[i] : 0.0;
-      const double sij = Qc.sd[i] * Qc.sd[j];
-      lch[i][j] = diag - sij * so;
-      ap[i][j] = diag - sij * se;
+#pragma unroll
+      for (int i = 0; i < NN; ++i)
+#pragma unroll
+        for (int j = i; j < NN; ++j) {
+          ap[i][j] = fma(ue[i], Qc.pt[le][j], ap[i][j]);
+          lch[i][j] = fma(uo[i], Qc.pt[lo][j], lch[i][j]);
+        }
     }
   }
+#pragma unroll
+  for (int i = 0; i < NN; ++i)
+#pragma unroll
+    for (int j = i; j < NN; ++j) {
+      const double diag = (i == j) ? Qc.rmu[i] : 0.0;
+      const double sij = Qc.sd[i] * Qc.sd[j];
+      lch[i][j] = fma(-sij, lch[i][j], diag);
+      ap[i][j] = fma(-sij, ap[i][j], diag);
+    }
   // L L^T = -A-  (lower triangle of lch)
-  if (!chol_inplace<NN>(lch)) st |= kStEigen;
+  double rdl[NN];
+  if (!chol_inplace<NN>(lch, rdl)) st |= kStEigen;
 
   // ---- pre-Jacobi vectors (depend on L only) ----
-  // beam: y2 = L^-1 W D^-1/2 rv, rv = -(M D^1/2)^-1 L L^T D^1/2 xs + M^-1 xd/mu0
-  //       lxd = D^1/2 L^-T L^-1 D^1/2 xd  (so that linv(xd) = lxd / w)
+  // beam: y2 = L^-1 W D^-1/2 rv, rv = -(M D^1/2)^-1 L L^T D^1/2 xs + M^-1 xd/mu0,
+  //       lxd = L^-T L^-1 D^1/2 xd  (linv(xd) = (sd/w) lxd)
   double y2[NN], lxd[NN];
+  const double fb2 = fb * (0.5 / kPi);
   if (beam) {
     double y[NN], z[NN];
 #pragma unroll
-    for (int i = 0; i < NN; ++i) y[i] = Qc.sd[i] * xs[i];
+    for (int i = 0; i < NN; ++i) y[i] = Qc.sd[i] * (fb2 * xs[i]);
 #pragma unroll
     for (int i = 0; i < NN; ++i) {  // z = L^T y
       double t = 0.0;
 #pragma unroll
-      for (int k = i; k < NN; ++k) t += lch[k][i] * y[k];
+      for (int k = i; k < NN; ++k) t = fma(lch[k][i], y[k], t);
       z[i] = t;
     }
 #pragma unroll
     for (int i = 0; i < NN; ++i) {  // y = L z
       double t = 0.0;
 #pragma unroll
-      for (int k = 0; k <= i; ++k) t += lch[i][k] * z[k];
+      for (int k = 0; k <= i; ++k) t = fma(lch[i][k], z[k], t);
       y[i] = t;
     }
 #pragma unroll
     for (int i = 0; i < NN; ++i) {
-      const double rv = (-y[i] / Qc.sd[i] + xd[i] * rmu0) / Qc.mu[i];
-      y2[i] = Qc.w[i] / Qc.sd[i] * rv;
-      lxd[i] = Qc.sd[i] * xd[i];
+      // rv = (-y/sd + xd/mu0)/mu, with 1/(sd mu) = 1/g; W D^-1/2 = diag(w/sd) = diag(g)
+      const double xdi = -fb2 * xd[i];
+      const double rv = fma(-y[i], Qc.rg[i], xdi * rmu0 * Qc.rmu[i]);
+      y2[i] = Qc.g[i] * rv;
+      lxd[i] = Qc.sd[i] * xdi;
     }
-    lower_solve<NN>(lch, y2);
-    lower_solve<NN>(lch, lxd);
-    lower_t_solve<NN>(lch, lxd);
-#pragma unroll
-    for (int i = 0; i < NN; ++i) lxd[i] *= Qc.sd[i];
+    lower_solve<NN>(lch, rdl, y2);
+    lower_solve<NN>(lch, rdl, lxd);   // lxd = L^-T L^-1 D^1/2 xd
+    lower_t_solve<NN>(lch, rdl, lxd);
   } else {
 #pragma unroll
     for (int i = 0; i < NN; ++i) y2[i] = lxd[i] = 0.0;
@@ -214,10 +240,10 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
     const double b1 = taup > 0.0 ? 2.0 * db / taup : 0.0;
 #pragma unroll
     for (int i = 0; i < NN; ++i) cvec[i] = Qc.sd[i] * Qc.mu[i];
-    lower_solve<NN>(lch, cvec);
-    lower_t_solve<NN>(lch, cvec);
+    lower_solve<NN>(lch, rdl, cvec);
+    lower_t_solve<NN>(lch, rdl, cvec);
 #pragma unroll
-    for (int i = 0; i < NN; ++i) cvec[i] = db + b1 * Qc.sd[i] / Qc.w[i] * cvec[i];
+    for (int i = 0; i < NN; ++i) cvec[i] = fma(b1 * Qc.rg[i], cvec[i], db);
   } else {
 #pragma unroll
     for (int i = 0; i < NN; ++i) cvec[i] = 0.0;
@@ -232,14 +258,14 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
     for (int i = 0; i < NN; ++i) {
       double t = 0.0;
 #pragma unroll
-      for (int k = j; k < NN; ++k) t += HD_SYM(ap, i, k) * lch[k][j];
+      for (int k = j; k < NN; ++k) t = fma(HD_SYM(ap, i, k), lch[k][j], t);
       mcol[i] = t;
     }
 #pragma unroll
     for (int i = 0; i <= j; ++i) {
       double t = 0.0;
 #pragma unroll
-      for (int k = i; k < NN; ++k) t += lch[k][i] * mcol[k];
+      for (int k = i; k < NN; ++k) t = fma(lch[k][i], mcol[k], t);
       sym[i][j] = t;
     }
   }
@@ -265,8 +291,8 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
     for (int j = 0; j < NN; ++j) {  // tt = V^T y2 / (1/mu0^2 - k^2)
       double t = 0.0;
 #pragma unroll
-      for (int i = 0; i < NN; ++i) t += v[i][j] * y2[i];
-      double den = r2 - kk[j] * kk[j];
+      for (int i = 0; i < NN; ++i) t = fma(v[i][j], y2[i], t);
+      double den = fma(-kk[j], kk[j], r2);
       if (fabs(den) < 1.0e-9 * r2) {
         st |= kStResonance;
         den = den < 0.0 ? -1.0e-9 * r2 : 1.0e-9 * r2;
@@ -278,34 +304,26 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
     for (int i = 0; i < NN; ++i) {  // y = V tt
       double t = 0.0;
 #pragma unroll
-      for (int j = 0; j < NN; ++j) t += v[i][j] * tt[j];
+      for (int j = 0; j < NN; ++j) t = fma(v[i][j], tt[j], t);
       y[i] = t;
     }
 #pragma unroll
     for (int i = 0; i < NN; ++i) {  // s = W^-1 D^1/2 L y
       double t = 0.0;
 #pragma unroll
-      for (int k = 0; k <= i; ++k) t += lch[i][k] * y[k];
-      sv[i] = Qc.sd[i] / Qc.w[i] * t;
+      for (int k = 0; k <= i; ++k) t = fma(lch[i][k], y[k], t);
+      sv[i] = Qc.rg[i] * t;
     }
-    // dd = linv(xd - mu s / mu0) = (lxd - D^1/2 L^-T L^-1 D^1/2 (mu s)/mu0) / w
+    // dd = (lxd - D^1/2 L^-T L^-1 D^1/2 (mu s) / mu0) / w
 #pragma unroll
     for (int i = 0; i < NN; ++i) y[i] = Qc.sd[i] * Qc.mu[i] * sv[i];
-    lower_solve<NN>(lch, y);
-    lower_t_solve<NN>(lch, y);
-    // cumulative scaled optical depth of the layers above
-    double tauc = 0.0;
-    for (int l2 = 0; l2 < lc; ++l2) {
-      const double* q2 = A.prop + ((size_t)s * L + (L - 1 - l2)) * np;
-      double a2 = np > 1 ? q2[1] : 0.0;
-      if (a2 == 1.0) a2 = 1.0 - kDither;
-      const double f2 = nm >= N ? q2[1 + N] : 0.0;
-      tauc += (1.0 - a2 * f2) * q2[0];
-    }
+    lower_solve<NN>(lch, rdl, y);
+    lower_t_solve<NN>(lch, rdl, y);
+    const double tauc = A.tauc[(size_t)lc * A.nsc + sl];  // scaled depth of layer top
     const double att = 0.5 * exp(-tauc * rmu0);
 #pragma unroll
     for (int i = 0; i < NN; ++i) {
-      const double dd = (lxd[i] - Qc.sd[i] * y[i] * rmu0) / Qc.w[i];
+      const double dd = Qc.rg[i] * fma(-y[i], rmu0, lxd[i]);  // (sd/w)(lxd - y/mu0)
       zp[i] = (sv[i] + dd) * att;
       zm[i] = (sv[i] - dd) * att;
     }
@@ -323,18 +341,18 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
     const double x = kk[j] * taup;
     const double e = exp(-x);
     const double m = -expm1(-x);
-    const double th = m / (1.0 + e);
-    const double delta = x > 1.0e-8 ? th / kk[j] : 0.5 * taup;
+    const double th = m * rcp_nr(1.0 + e);
+    const double delta = x > 1.0e-8 ? th * rcp_nr(kk[j] > 0.0 ? kk[j] : 1.0) : 0.5 * taup;
     dsq[j] = sqrt(delta);
     gsq[j] = sqrt(kk[j] * th);
   }
-  // Psi^T = L^-T V Gamma^1/2 -> LDS (one column of 8 doubles per lane at a time)
+  // Psi^T = L^-T V Gamma^1/2 -> LDS (one column per step)
 #pragma unroll
   for (int j = 0; j < NN; ++j) {
     double x[NN];
 #pragma unroll
     for (int i = 0; i < NN; ++i) x[i] = v[i][j];
-    lower_t_solve<NN>(lch, x);
+    lower_t_solve<NN>(lch, rdl, x);
 #pragma unroll
     for (int i = 0; i < NN; ++i) psi_lds[(i * NN + j) * kLayerBlock + lt] = x[i] * gsq[j];
   }
@@ -345,7 +363,7 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
     for (int j = 0; j < NN; ++j) {
       double t = 0.0;
 #pragma unroll
-      for (int a = 0; a <= i; ++a) t += lch[i][a] * v[a][j];
+      for (int a = 0; a <= i; ++a) t = fma(lch[i][a], v[a][j], t);
       v[i][j] = t * dsq[j];
     }
 
@@ -355,25 +373,25 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
   double ga[NN], gb[NN];
 #pragma unroll
   for (int i = 0; i < NN; ++i) {
-    ga[i] = Qc.g[i] * (cvec[i] - (zm[i] - zp[i] * e0));
-    gb[i] = Qc.g[i] * (zm[i] + zp[i] * e0 + bsum);
+    ga[i] = Qc.g[i] * (cvec[i] - fma(-zp[i], e0, zm[i]));
+    gb[i] = Qc.g[i] * (fma(zp[i], e0, zm[i]) + bsum);
   }
   // Q~- = Omega (I + Omega^T Omega)^-1 Omega^T = Phi Phi^T, Phi = Omega J^-T
   double pvec[NN];
   {
-    double hm[NN][NN];
+    double hm[NN][NN], rdh[NN];
 #pragma unroll
     for (int i = 0; i < NN; ++i)
 #pragma unroll
       for (int j = i; j < NN; ++j) {
         double t = (i == j) ? 1.0 : 0.0;
 #pragma unroll
-        for (int k = 0; k < NN; ++k) t += v[k][i] * v[k][j];
+        for (int k = 0; k < NN; ++k) t = fma(v[k][i], v[k][j], t);
         hm[i][j] = t;
       }
-    if (!chol_inplace<NN>(hm)) st |= kStEigen;
+    if (!chol_inplace<NN>(hm, rdh)) st |= kStEigen;
 #pragma unroll
-    for (int r = 0; r < NN; ++r) lower_solve<NN>(hm, v[r]);
+    for (int r = 0; r < NN; ++r) lower_solve<NN>(hm, rdh, v[r]);
     // Q~- (upper) -> temporarily into the R~ slot; p = Q~- ga
 #pragma unroll
     for (int i = 0; i < NN; ++i) pvec[i] = 0.0;
@@ -384,10 +402,10 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
       for (int j = i; j < NN; ++j) {
         double t = 0.0;
 #pragma unroll
-        for (int k = 0; k < NN; ++k) t += v[i][k] * v[j][k];
+        for (int k = 0; k < NN; ++k) t = fma(v[i][k], v[j][k], t);
         out[(e++) * so] = t;
-        pvec[i] += t * ga[j];
-        if (j != i) pvec[j] += t * ga[i];
+        pvec[i] = fma(t, ga[j], pvec[i]);
+        if (j != i) pvec[j] = fma(t, ga[i], pvec[j]);
       }
   }
   // Q~+ = -Psi^T (I + Psi Psi^T)^-1 Psi = -Xi^T Xi, Xi = J+^-1 Psi
@@ -398,26 +416,26 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
     for (int i = 0; i < NN; ++i)
 #pragma unroll
       for (int j = 0; j < NN; ++j) pt_[i][j] = psi_lds[(i * NN + j) * kLayerBlock + lt];
-    double hp[NN][NN];
+    double hp[NN][NN], rdh[NN];
 #pragma unroll
     for (int i = 0; i < NN; ++i)
 #pragma unroll
       for (int j = i; j < NN; ++j) {
         double t = (i == j) ? 1.0 : 0.0;
 #pragma unroll
-        for (int k = 0; k < NN; ++k) t += pt_[k][i] * pt_[k][j];
+        for (int k = 0; k < NN; ++k) t = fma(pt_[k][i], pt_[k][j], t);
         hp[i][j] = t;
       }
-    if (!chol_inplace<NN>(hp)) st |= kStEigen;
+    if (!chol_inplace<NN>(hp, rdh)) st |= kStEigen;
 #pragma unroll
-    for (int r = 0; r < NN; ++r) lower_solve<NN>(hp, pt_[r]);
+    for (int r = 0; r < NN; ++r) lower_solve<NN>(hp, rdh, pt_[r]);
 #pragma unroll
     for (int i = 0; i < NN; ++i)
 #pragma unroll
       for (int j = i; j < NN; ++j) {
         double t = 0.0;
 #pragma unroll
-        for (int k = 0; k < NN; ++k) t += pt_[i][k] * pt_[j][k];
+        for (int k = 0; k < NN; ++k) t = fma(pt_[i][k], pt_[j][k], t);
         qp[i][j] = -t;
       }
   }
@@ -426,7 +444,7 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
   for (int i = 0; i < NN; ++i) {
     double t = 0.0;
 #pragma unroll
-    for (int j = 0; j < NN; ++j) t += HD_SYM(qp, i, j) * gb[j];
+    for (int j = 0; j < NN; ++j) t = fma(HD_SYM(qp, i, j), gb[j], t);
     qvec[i] = t;
   }
 
@@ -505,8 +523,17 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
   for (int lc = 0; lc < L; ++lc) {
     const double* lp = A.scr + (size_t)lc * ne1<NN>() * nsc + sl;
     double* bp = A.bsub + (size_t)lc * ne2<NN>() * nsc + sl;
-#define RL(i, j) lp[(size_t)sym_index<NN>(i, j) * nsc]
-#define TL(i, j) lp[(size_t)(nsym + sym_index<NN>(i, j)) * nsc]
+    // this layer's R~ (upper) and S~+ ; each record element is read once
+    double rl[NN][NN], spl[NN];
+    {
+      int e = 0;
+#pragma unroll
+      for (int i = 0; i < NN; ++i)
+#pragma unroll
+        for (int j = i; j < NN; ++j) rl[i][j] = lp[(size_t)(e++) * nsc];
+#pragma unroll
+      for (int i = 0; i < NN; ++i) spl[i] = lp[(size_t)(2 * nsym + i) * nsc];
+    }
 
     // level lc (top of layer lc): F_dn = rc . I+ + cs
     {
@@ -515,13 +542,13 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
       for (int i = 0; i < NN; ++i) {
         double t = 0.0;
 #pragma unroll
-        for (int j = 0; j < NN; ++j) t += HD_SYM(ra, j, i) * Qc.g[j];
-        bp[(NN * NN + NN + i) * nsc] = twopi * t;
-        cs += Qc.g[i] * sd[i];
+        for (int j = 0; j < NN; ++j) t = fma(HD_SYM(ra, j, i), Qc.g[j], t);
+        bp[(size_t)(NN * NN + NN + i) * nsc] = twopi * t;
+        cs = fma(Qc.g[i], sd[i], cs);
       }
-      bp[(NN * NN + 2 * NN) * nsc] = twopi * cs + f0mu0 * exp(-tauc * rmu0);
+      bp[(size_t)(NN * NN + 2 * NN) * nsc] = fma(twopi, cs, f0mu0 * exp(-tauc * rmu0));
     }
-
+    HD_PHASE();
     // A = Ra (full); W1 = I - R_l A ; v1 = R_l Sd + S+
     double am[NN][NN], w1[NN][NN], t1[NN];
 #pragma unroll
@@ -530,45 +557,44 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
       for (int j = 0; j < NN; ++j) am[i][j] = HD_SYM(ra, i, j);
 #pragma unroll
     for (int i = 0; i < NN; ++i) {
-      double rrow[NN];
-#pragma unroll
-      for (int k = 0; k < NN; ++k) rrow[k] = RL(i, k);
 #pragma unroll
       for (int j = 0; j < NN; ++j) {
         double t = (i == j) ? 1.0 : 0.0;
 #pragma unroll
-        for (int k = 0; k < NN; ++k) t -= rrow[k] * am[k][j];
+        for (int k = 0; k < NN; ++k) t = fma(-HD_SYM(rl, i, k), am[k][j], t);
         w1[i][j] = t;
       }
-      double t = lp[(2 * nsym + i) * nsc];
+      double t = spl[i];
 #pragma unroll
-      for (int k = 0; k < NN; ++k) t += rrow[k] * sd[k];
+      for (int k = 0; k < NN; ++k) t = fma(HD_SYM(rl, i, k), sd[k], t);
       t1[i] = t;
     }
-    // LU without pivoting (W1 = I - product of reflections; pivot watch)
+    HD_PHASE();
+    // LU without pivoting (W1 = I - product of reflections; pivot watch);
+    // reciprocal pivots kept on the diagonal
 #pragma unroll
     for (int k = 0; k < NN; ++k) {
       const double piv = w1[k][k];
       if (!(fabs(piv) > 1.0e-12)) st |= kStPivot;
-      const double rp = 1.0 / piv;
-      w1[k][k] = rp;  // reciprocal kept on the diagonal
+      const double rp = rcp_nr(piv);
+      w1[k][k] = rp;
 #pragma unroll
       for (int i = k + 1; i < NN; ++i) {
         const double l = w1[i][k] * rp;
         w1[i][k] = l;
 #pragma unroll
-        for (int j = k + 1; j < NN; ++j) w1[i][j] -= l * w1[k][j];
+        for (int j = k + 1; j < NN; ++j) w1[i][j] = fma(-l, w1[k][j], w1[i][j]);
       }
     }
     // t = W1^-1 v1
 #pragma unroll
     for (int i = 0; i < NN; ++i)
 #pragma unroll
-      for (int k = 0; k < i; ++k) t1[i] -= w1[i][k] * t1[k];
+      for (int k = 0; k < i; ++k) t1[i] = fma(-w1[i][k], t1[k], t1[i]);
 #pragma unroll
     for (int i = NN - 1; i >= 0; --i) {
 #pragma unroll
-      for (int k = i + 1; k < NN; ++k) t1[i] -= w1[i][k] * t1[k];
+      for (int k = i + 1; k < NN; ++k) t1[i] = fma(-w1[i][k], t1[k], t1[i]);
       t1[i] *= w1[i][i];
     }
     // u = A t + Sd
@@ -577,10 +603,11 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
     for (int i = 0; i < NN; ++i) {
       double t = sd[i];
 #pragma unroll
-      for (int k = 0; k < NN; ++k) t += am[i][k] * t1[k];
+      for (int k = 0; k < NN; ++k) t = fma(am[i][k], t1[k], t);
       u[i] = t;
-      bp[(NN * NN + i) * nsc] = t1[i];
+      bp[(size_t)(NN * NN + i) * nsc] = t1[i];
     }
+    HD_PHASE();
     // M1 = A W1^-1, row-wise in place:  x W1 = a  ->  (x L) U = a
 #pragma unroll
     for (int r = 0; r < NN; ++r) {
@@ -588,42 +615,47 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
       for (int j = 0; j < NN; ++j) {  // z U = a  (forward over columns)
         double t = am[r][j];
 #pragma unroll
-        for (int k = 0; k < j; ++k) t -= am[r][k] * w1[k][j];
+        for (int k = 0; k < j; ++k) t = fma(-am[r][k], w1[k][j], t);
         am[r][j] = t * w1[j][j];
       }
 #pragma unroll
       for (int j = NN - 1; j >= 0; --j) {  // x L = z  (backward, unit L)
         double t = am[r][j];
 #pragma unroll
-        for (int k = j + 1; k < NN; ++k) t -= am[r][k] * w1[k][j];
+        for (int k = j + 1; k < NN; ++k) t = fma(-am[r][k], w1[k][j], t);
         am[r][j] = t;
       }
     }
-    // ZT = W1^-1 T_l (stored column by column)
+    HD_PHASE();
+    // T~ (upper), read once; ZT = W1^-1 T_l stored column by column
+    double tl[NN][NN];
+    {
+      int e = nsym;
+#pragma unroll
+      for (int i = 0; i < NN; ++i)
+#pragma unroll
+        for (int j = i; j < NN; ++j) tl[i][j] = lp[(size_t)(e++) * nsc];
+    }
 #pragma unroll
     for (int j = 0; j < NN; ++j) {
       double x[NN];
 #pragma unroll
-      for (int i = 0; i < NN; ++i) x[i] = TL(i, j);
+      for (int i = 0; i < NN; ++i) x[i] = HD_SYM(tl, i, j);
 #pragma unroll
       for (int i = 0; i < NN; ++i)
 #pragma unroll
-        for (int k = 0; k < i; ++k) x[i] -= w1[i][k] * x[k];
+        for (int k = 0; k < i; ++k) x[i] = fma(-w1[i][k], x[k], x[i]);
 #pragma unroll
       for (int i = NN - 1; i >= 0; --i) {
 #pragma unroll
-        for (int k = i + 1; k < NN; ++k) x[i] -= w1[i][k] * x[k];
+        for (int k = i + 1; k < NN; ++k) x[i] = fma(-w1[i][k], x[k], x[i]);
         x[i] *= w1[i][i];
       }
 #pragma unroll
-      for (int i = 0; i < NN; ++i) bp[(i * NN + j) * nsc] = x[i];
+      for (int i = 0; i < NN; ++i) bp[(size_t)(i * NN + j) * nsc] = x[i];
     }
+    HD_PHASE();
     // P = M1 T_l (row-wise in place)
-    double tl[NN][NN];
-#pragma unroll
-    for (int i = 0; i < NN; ++i)
-#pragma unroll
-      for (int j = i; j < NN; ++j) tl[i][j] = TL(i, j);
 #pragma unroll
     for (int r = 0; r < NN; ++r) {
       double row[NN];
@@ -631,30 +663,29 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
       for (int j = 0; j < NN; ++j) {
         double t = 0.0;
 #pragma unroll
-        for (int k = 0; k < NN; ++k) t += am[r][k] * HD_SYM(tl, k, j);
+        for (int k = 0; k < NN; ++k) t = fma(am[r][k], HD_SYM(tl, k, j), t);
         row[j] = t;
       }
 #pragma unroll
       for (int j = 0; j < NN; ++j) am[r][j] = row[j];
     }
+    HD_PHASE();
     // Ra <- R_l + T_l P (upper) ; Sd <- T_l u + S-
 #pragma unroll
     for (int i = 0; i < NN; ++i) {
 #pragma unroll
       for (int j = i; j < NN; ++j) {
-        double t = RL(i, j);
+        double t = rl[i][j];
 #pragma unroll
-        for (int k = 0; k < NN; ++k) t += HD_SYM(tl, i, k) * am[k][j];
+        for (int k = 0; k < NN; ++k) t = fma(HD_SYM(tl, i, k), am[k][j], t);
         ra[i][j] = t;
       }
-      double t = lp[(2 * nsym + NN + i) * nsc];
+      double t = lp[(size_t)(2 * nsym + NN + i) * nsc];
 #pragma unroll
-      for (int k = 0; k < NN; ++k) t += HD_SYM(tl, i, k) * u[k];
+      for (int k = 0; k < NN; ++k) t = fma(HD_SYM(tl, i, k), u[k], t);
       sd[i] = t;
     }
-    tauc += lp[(2 * nsym + 2 * NN) * nsc];
-#undef RL
-#undef TL
+    tauc += lp[(size_t)(2 * nsym + 2 * NN) * nsc];
   }
 
   // ---- Lambertian surface: I+ = g x ----
@@ -728,6 +759,8 @@ static void fill_quad(Quad<NN>& q, const QuadHost& h) {
     q.w[i] = h.w[i];
     q.sd[i] = h.sd[i];
     q.g[i] = h.g[i];
+    q.rmu[i] = 1.0 / h.mu[i];
+    q.rg[i] = 1.0 / h.g[i];
     for (int l = 0; l < 2 * NN; ++l) q.pt[l][i] = h.pt[l][i];
   }
 }
@@ -746,8 +779,12 @@ hipError_t upload_quad_tables(const QuadHost* per_nn /* [kMaxNN], index nn-1 */)
 }
 
 template <int NN>
-static hipError_t launch_chunk(const PlanckArgs* pa, const LayerArgs& la, const SweepArgs& sa,
-                               hipStream_t stream, hipEvent_t* ev) {
+static hipError_t launch_chunk(const PlanckArgs* pa, const TaucArgs* ta, const LayerArgs& la,
+                               const SweepArgs& sa, hipStream_t stream, hipEvent_t* ev) {
+  if (ta) {
+    hipLaunchKernelGGL(hd_tauc_kernel, dim3((unsigned)((ta->nsc + 255) / 256)), dim3(256), 0,
+                       stream, *ta);
+  }
   if (pa) {
     const long n0 = (long)pa->nsc * (pa->nlyr + 3);
     hipLaunchKernelGGL(hd_planck_kernel, dim3((unsigned)((n0 + 255) / 256)), dim3(256), 0,
@@ -764,17 +801,18 @@ static hipError_t launch_chunk(const PlanckArgs* pa, const LayerArgs& la, const 
   return hipGetLastError();
 }
 
-hipError_t launch_solve_chunk_nn(int nn, const PlanckArgs* pa, const LayerArgs& la,
-                                 const SweepArgs& sa, hipStream_t stream, hipEvent_t* ev) {
+hipError_t launch_solve_chunk_nn(int nn, const PlanckArgs* pa, const TaucArgs* ta,
+                                 const LayerArgs& la, const SweepArgs& sa, hipStream_t stream,
+                                 hipEvent_t* ev) {
   switch (nn) {
-    case 1: return launch_chunk<1>(pa, la, sa, stream, ev);
-    case 2: return launch_chunk<2>(pa, la, sa, stream, ev);
-    case 3: return launch_chunk<3>(pa, la, sa, stream, ev);
-    case 4: return launch_chunk<4>(pa, la, sa, stream, ev);
-    case 5: return launch_chunk<5>(pa, la, sa, stream, ev);
-    case 6: return launch_chunk<6>(pa, la, sa, stream, ev);
-    case 7: return launch_chunk<7>(pa, la, sa, stream, ev);
-    case 8: return launch_chunk<8>(pa, la, sa, stream, ev);
+    case 1: return launch_chunk<1>(pa, ta, la, sa, stream, ev);
+    case 2: return launch_chunk<2>(pa, ta, la, sa, stream, ev);
+    case 3: return launch_chunk<3>(pa, ta, la, sa, stream, ev);
+    case 4: return launch_chunk<4>(pa, ta, la, sa, stream, ev);
+    case 5: return launch_chunk<5>(pa, ta, la, sa, stream, ev);
+    case 6: return launch_chunk<6>(pa, ta, la, sa, stream, ev);
+    case 7: return launch_chunk<7>(pa, ta, la, sa, stream, ev);
+    case 8: return launch_chunk<8>(pa, ta, la, sa, stream, ev);
     default: return hipErrorInvalidValue;
   }
 }
@@ -782,7 +820,7 @@ hipError_t launch_solve_chunk_nn(int nn, const PlanckArgs* pa, const LayerArgs& 
 size_t scratch_doubles_per_solve(int nn, int nlyr, bool planck) {
   const size_t ne1 = (size_t)(nn * (nn + 1) + 2 * nn + 1);
   const size_t ne2 = (size_t)(nn * nn + 2 * nn + 1);
-  return (ne1 + ne2) * nlyr + (planck ? (size_t)nlyr + 3 : 0);
+  return (ne1 + ne2) * nlyr + (planck ? (size_t)nlyr + 3 : 0) + (size_t)nlyr;  // + tauc
 }
 
 }  // namespace hd

@@ -37,8 +37,20 @@ struct PlanckArgs {
   int nlyr;
 };
 
+struct TaucArgs {
+  const double* prop;
+  double* out;  // [nlyr][nsc] scaled optical depth at the top of each solver layer
+  long s0;
+  int nsc;
+  int nlyr;
+  int nprop;
+  int use_f;    // delta-M active (moments >= nstr available)
+  int f_slot;   // prop slot of chi_nstr = 1 + nstr
+};
+
 struct LayerArgs {
   const double* prop;
+  const double* tauc;     // [nlyr][nsc] (beam) or null
   const double* fbeam;
   const double* umu0;
   const double* planckv;  // [nlyr+3][nsc] (planck) or null
@@ -81,8 +93,9 @@ struct QuadHost {
 // copy the quadrature tables (index nn-1) into the current device's constant memory
 hipError_t upload_quad_tables(const QuadHost* per_nn);
 // ev: 3 events (before K1, between, after K2) or nullptr; pa null when planck is off
-hipError_t launch_solve_chunk_nn(int nn, const PlanckArgs* pa, const LayerArgs& la,
-                                 const SweepArgs& sa, hipStream_t stream, hipEvent_t* ev);
+hipError_t launch_solve_chunk_nn(int nn, const PlanckArgs* pa, const TaucArgs* ta,
+                                 const LayerArgs& la, const SweepArgs& sa, hipStream_t stream,
+                                 hipEvent_t* ev);
 size_t scratch_doubles_per_solve(int nn, int nlyr, bool planck);
 
 }  // namespace hd
