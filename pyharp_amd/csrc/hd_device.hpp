@@ -268,7 +268,7 @@ __device__ __forceinline__ void jacobi_eig(double (&a)[NN][NN], double (&v)[NN][
 #pragma unroll
         for (int j = i + 1; j < NN; ++j) off = fma(a[i][j], a[i][j], off);
       }
-      const bool done = !(off > 1.0e-34 * dia);
+      const bool done = !(off > 1.0e-30 * dia);  // off-diagonal <~ 1e-15 relative
       if (__all(done)) break;
 #pragma unroll
       for (int r = 0; r < P - 1; ++r) jacobi_round<NN>(r, a, v, !done);

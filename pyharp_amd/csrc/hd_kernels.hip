@@ -339,9 +339,8 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
 #pragma unroll
   for (int j = 0; j < NN; ++j) {
     const double x = kk[j] * taup;
-    const double e = exp(-x);
-    const double m = -expm1(-x);
-    const double th = m * rcp_nr(1.0 + e);
+    const double m = -expm1(-x);           // 1 - exp(-k tau')
+    const double th = m * rcp_nr(2.0 - m);  // tanh(k tau'/2)
     const double delta = x > 1.0e-8 ? th * rcp_nr(kk[j] > 0.0 ? kk[j] : 1.0) : 0.5 * taup;
     dsq[j] = sqrt(delta);
     gsq[j] = sqrt(kk[j] * th);
@@ -377,7 +376,7 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
     gb[i] = Qc.g[i] * (fma(zp[i], e0, zm[i]) + bsum);
   }
   // Q~- = Omega (I + Omega^T Omega)^-1 Omega^T = Phi Phi^T, Phi = Omega J^-T
-  double pvec[NN];
+  double pvec[NN], qmr[NN][NN];
   {
     double hm[NN][NN], rdh[NN];
 #pragma unroll
@@ -392,10 +391,9 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
     if (!chol_inplace<NN>(hm, rdh)) st |= kStEigen;
 #pragma unroll
     for (int r = 0; r < NN; ++r) lower_solve<NN>(hm, rdh, v[r]);
-    // Q~- (upper) -> temporarily into the R~ slot; p = Q~- ga
+    // Q~- (upper, kept in registers); p = Q~- ga
 #pragma unroll
     for (int i = 0; i < NN; ++i) pvec[i] = 0.0;
-    int e = 0;
 #pragma unroll
     for (int i = 0; i < NN; ++i)
 #pragma unroll
@@ -403,7 +401,7 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
         double t = 0.0;
 #pragma unroll
         for (int k = 0; k < NN; ++k) t = fma(v[i][k], v[j][k], t);
-        out[(e++) * so] = t;
+        qmr[i][j] = t;
         pvec[i] = fma(t, ga[j], pvec[i]);
         if (j != i) pvec[j] = fma(t, ga[i], pvec[j]);
       }
@@ -456,7 +454,7 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
     for (int i = 0; i < NN; ++i)
 #pragma unroll
       for (int j = i; j < NN; ++j) {
-        const double qm = out[e * so];
+        const double qm = qmr[i][j];
         const double r = qm + qp[i][j];
         const double t = ((i == j) ? 1.0 : 0.0) - qm + qp[i][j];
         out[e * so] = r;
