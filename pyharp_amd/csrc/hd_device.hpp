@@ -209,15 +209,21 @@ __device__ __forceinline__ void jacobi_round(int r, double (&a)[NN][NN], double 
     const int x = tour_a(P, r, k), y = tour_b(P, r, k);
     const int p = x < y ? x : y, q = x < y ? y : x;
     if (q >= NN) continue;
+    // with w = sqrt(d^2 + 4 a^2), u = |d| + w, z = 1/sqrt(2 w u):
+    //   c = u z,  s = sgn(d) 2 a z,  t = s/c = sgn(d) 2a/u = sgn(d) 4 a w z^2
+    // (the standard t = sgn(theta)/(|theta| + sqrt(theta^2+1)), theta = d/2a)
     const double apq = a[p][q];
     const double d = a[q][q] - a[p][p];
-    const double den = fabs(d) + sqrt(fma(d, d, 4.0 * apq * apq));
-    double t = (den > 0.0 && on) ? 2.0 * apq * rcp_nr(den > 0.0 ? den : 1.0) : 0.0;
-    t = d < 0.0 ? -t : t;
-    const double c = rsq_nr(fma(t, t, 1.0));
-    cc[k] = c;
-    ss[k] = t * c;
-    tt[k] = t;
+    const double w2 = fma(d, d, 4.0 * apq * apq);
+    const bool rot = on && w2 > 1.0e-280;
+    const double w2s = rot ? w2 : 1.0;
+    const double w = w2s * rsq_nr(w2s);
+    const double u = fabs(d) + w;
+    const double z = rsq_nr(2.0 * w * u);
+    const double sg = d < 0.0 ? -2.0 : 2.0;
+    cc[k] = rot ? u * z : 1.0;
+    ss[k] = rot ? sg * apq * z : 0.0;
+    tt[k] = rot ? sg * apq * (2.0 * w) * (z * z) : 0.0;
   }
 #pragma unroll
   for (int k = 0; k < H; ++k) {

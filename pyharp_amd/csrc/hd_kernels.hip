@@ -49,6 +49,7 @@ __device__ __forceinline__ const Quad<NN>& quad() {
 }
 
 constexpr int kLayerBlock = 256;
+constexpr int kLayersPerBlock = kLayerBlock / 64;
 
 // phase boundary: keeps the scheduler from hoisting the next phase's loads
 // (and their registers) above the current phase
@@ -107,13 +108,17 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
   constexpr int kPsi = NN > 1 ? NN * NN : 1;
   __shared__ double psi_lds[kPsi * kLayerBlock];  // Psi^T staged per lane
   const Quad<NN>& Qc = quad<NN>();
-  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long ntot = (long)A.nsc * A.nlyr;
-  if (tid >= ntot) return;
+  // block = 64 consecutive solves (one wave each) x kLayersPerBlock consecutive
+  // layers: a wave's stores are coalesced (same layer, consecutive solves) and
+  // the block's waves read neighbouring records of the same solves (shared lines)
   const int lt = threadIdx.x;
+  const int ntile_s = (A.nsc + 63) / 64;
+  const int ts = blockIdx.x % ntile_s;
+  const int tl = blockIdx.x / ntile_s;
+  const int sl = ts * 64 + (lt & 63);
+  const int lc = tl * kLayersPerBlock + (lt >> 6);  // solver layer, 0 = top
   const int L = A.nlyr;
-  const int lc = (int)(tid / A.nsc);  // solver layer, 0 = top
-  const int sl = (int)(tid - (long)lc * A.nsc);
+  if (sl >= A.nsc || lc >= L) return;
   const long s = A.s0 + sl;
   const int nm = A.nmom;
   const int np = A.nprop;
@@ -788,8 +793,8 @@ static hipError_t launch_chunk(const PlanckArgs* pa, const TaucArgs* ta, const L
     hipLaunchKernelGGL(hd_planck_kernel, dim3((unsigned)((n0 + 255) / 256)), dim3(256), 0,
                        stream, *pa);
   }
-  const long ntot = (long)la.nsc * la.nlyr;
-  const unsigned nb1 = (unsigned)((ntot + kLayerBlock - 1) / kLayerBlock);
+  const unsigned nb1 = (unsigned)(((la.nsc + 63) / 64) *
+                                  ((la.nlyr + kLayersPerBlock - 1) / kLayersPerBlock));
   const unsigned nb2 = (unsigned)((la.nsc + 63) / 64);
   if (ev) (void)hipEventRecord(ev[0], stream);
   hipLaunchKernelGGL(hd_layer_kernel<NN>, dim3(nb1), dim3(kLayerBlock), 0, stream, la);
