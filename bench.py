@@ -103,18 +103,19 @@ def wave_bounds(ngpoint):
     return lo, lo + 30.0
 
 
-def load_pmc(workload: str):
+def load_pmc(nstr: int, nlyr: int, planck: bool):
+    """Measured HBM bytes per solve per kernel (profiles/pmc_latest.json, scripts/pmc_summarize.py)."""
     p = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if not os.path.exists(p):
         return None
     try:
         with open(p) as f:
             d = json.load(f)
-        if d.get("workload") != workload:
-            return None
-        return d
-    except Exception:
+    except (OSError, ValueError):
         return None
+    if (d.get("nstr"), d.get("nlyr"), bool(d.get("planck"))) != (nstr, nlyr, bool(planck)):
+        return None
+    return d
 
 
 def cpu_baseline(prop, bc, temf, nstr, planck, wl, wu, target_s=12.0):
@@ -229,11 +230,21 @@ def main():
         k1_avg_ms = tm.layer_ms / max(tm.layer_launches, 1)
         solves_per_launch = W * ncol * args.steps / max(tm.layer_launches, 1)
         ach = k1_flop * solves_per_launch / (k1_avg_ms * 1e-3) / 1e12
-        pmc = load_pmc(workload)
+        pmc = load_pmc(nstr, nlyr, args.planck)
+        traffic = None
+        if pmc:
+            k1 = pmc["kernels"].get(f"hd_layer_kernel<{nstr // 2}>")
+            if k1:
+                traffic = round(k1["bytes_per_solve"] * solves_per_launch)
         roofline = {"bound": "mfma", "kernel": "hd_layer_kernel", "achieved": round(ach, 3),
                     "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(ach / FP64_PEAK_TFLOPS, 4),
-                    "traffic": (pmc or {}).get("layer_kernel_bytes_per_launch"),
+                    "traffic": traffic,
+                    "traffic_note": None if pmc is None else
+                    f"HBM bytes per launch from rocprofv3 PMC run {pmc['source']} "
+                    "(2 x FETCH_SIZE + WRITE_SIZE, scaled to this launch's solves); "
+                    "algorithmic bytes per solve are much smaller: the layer records "
+                    "(89 doubles per layer) are written to HBM scratch for the sweep",
                     "avg_launch_ms": round(k1_avg_ms, 3),
                     "flop_per_solve": k1_flop,
                     "note": "FP64 compute bound (gfx950 FP64 vector and MFMA peaks are equal); "

@@ -1,0 +1,65 @@
+"""Fold rocprofv3 FETCH_SIZE / WRITE_SIZE passes into profiles/pmc_latest.json.
+
+    python scripts/pmc_summarize.py gpurun_out/TAG [--solves 65536] [--nstr 16] [--nlyr 80]
+
+Inputs are the two separate `--pmc` passes written by scripts/gpu_check.sh over
+scripts/pmc_run.py (one 65 536-solve chunk of the C4 shape per launch).  Units:
+rocprofv3 reports both counters in KiB.  gfx950 correction
+(MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts half the bytes of a wide
+coalesced streaming read, so fetch is doubled; WRITE_SIZE is exact.  Our
+kernels' loads are 64 consecutive doubles per wave instruction; the doubling is
+confirmed on this access pattern by hd_sweep_kernel, whose algorithmic read
+bytes (layer records + back-substitution records) match 2 x FETCH_SIZE to 2 %.
+"""
+
+import argparse
+import csv
+import json
+import os
+
+
+def per_kernel(path, counter):
+    acc = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] != counter:
+                continue
+            name = r["Kernel_Name"]
+            if not name.startswith(("void hd::", "hd::")):
+                continue
+            key = name.split("(")[0].replace("void ", "").replace("hd::", "")
+            acc.setdefault(key, []).append(float(r["Counter_Value"]) * 1024.0)
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("run_dir")
+    ap.add_argument("--solves", type=int, default=65536)
+    ap.add_argument("--nstr", type=int, default=16)
+    ap.add_argument("--nlyr", type=int, default=80)
+    ap.add_argument("--planck", action="store_true")
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles",
+                                                   "pmc_latest.json"))
+    a = ap.parse_args()
+    fetch = per_kernel(os.path.join(a.run_dir, "pmc_fetch", "pmc_counter_collection.csv"),
+                       "FETCH_SIZE")
+    write = per_kernel(os.path.join(a.run_dir, "pmc_write", "pmc_counter_collection.csv"),
+                       "WRITE_SIZE")
+    kernels = {}
+    for k in sorted(set(fetch) | set(write)):
+        rd = 2.0 * fetch.get(k, 0.0)
+        wr = write.get(k, 0.0)
+        kernels[k] = {"fetch_bytes_raw": fetch.get(k), "read_bytes": rd, "write_bytes": wr,
+                      "bytes_per_launch": rd + wr, "bytes_per_solve": (rd + wr) / a.solves}
+    out = {"nstr": a.nstr, "nlyr": a.nlyr, "planck": bool(a.planck),
+           "solves_per_launch": a.solves, "source": os.path.basename(os.path.normpath(a.run_dir)),
+           "correction": "read = 2 x FETCH_SIZE (gfx950 half-count), write = WRITE_SIZE; KiB -> B",
+           "kernels": kernels}
+    with open(a.out, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
