@@ -108,8 +108,8 @@ class DisortImpl : public torch::nn::Cloneable<DisortImpl> {
     for (auto const& f : flags) TORCH_CHECK(known.count(f), "Disort: unknown flag ", f);
     TORCH_CHECK(flags.count("lamber"), "Disort: only Lambertian lower boundaries are supported");
     auto const& ds = options.ds();
-    TORCH_CHECK(ds.nstr >= 2 && ds.nstr % 2 == 0 && ds.nstr <= 16,
-                "Disort: nstr must be even and in [2, 16]");
+    TORCH_CHECK(ds.nstr >= 2 && ds.nstr % 2 == 0 && ds.nstr <= 32,
+                "Disort: nstr must be even and in [2, 32]");
     TORCH_CHECK(ds.nlyr >= 1, "Disort: nlyr must be >= 1");
     planck_ = flags.count("planck") > 0;
     if (planck_)

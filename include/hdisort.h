@@ -64,7 +64,7 @@ extern "C" {
 #define HD_STATUS_ERROR_MASK 0x0F
 
 typedef struct hd_config {
-  int nstr;       /* number of streams, even, 2..16 */
+  int nstr;       /* number of streams, even, 2..32 */
   int nmom;       /* phase moments the module was configured with (>= 0)   */
   int nlyr;       /* layers                                                 */
   int nprop;      /* last-dim size of prop (>= 1); moments used = min(nmom, nprop-2) */

@@ -13,7 +13,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libhdisort.so")
-SOURCES = ["hd_kernels.hip", "hd_api.cpp"]
+SOURCES = ["hd_kernels.hip", "hd_team.hip", "hd_api.cpp"]
 HEADERS = ["hd_device.hpp", "hd_kernels.hpp", os.path.join("..", "..", "include", "hdisort.h")]
 ARCH = os.environ.get("HD_OFFLOAD_ARCH", "gfx950")
 
@@ -38,15 +38,18 @@ def _stale() -> bool:
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return LIB
-    objs = []
-    for src in SOURCES:
+    objs, procs = [], []
+    for src in SOURCES:  # one hipcc per source, in parallel (the team TU dominates)
         obj = os.path.join(CSRC, src + ".o")
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
                "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
-        subprocess.run(cmd, check=True)
+        procs.append((cmd, subprocess.Popen(cmd)))
         objs.append(obj)
+    for cmd, p in procs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, cmd)
     tmp = LIB + ".tmp"
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     subprocess.run(cmd, check=True)

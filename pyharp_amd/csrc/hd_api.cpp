@@ -119,16 +119,21 @@ int ensure_tables(hd_context* ctx) {
   static hd::QuadHost all[hd::kMaxNN];
   for (int nn = 1; nn <= hd::kMaxNN; ++nn) make_quad(nn, all[nn - 1]);
   hipError_t e = hd::upload_quad_tables(all);
+  if (e == hipSuccess) e = hd::upload_quad_tables_team(all);
   if (e != hipSuccess) return fail(ctx, HD_EHIP, "hd_solve: constant upload: %s", hipGetErrorString(e));
   ctx->tables = true;
   return HD_OK;
 }
 
-long auto_chunk(long nsolve, int nlyr) {
-  // Enough solves per chunk to fill 256 CUs with the one-lane-per-solve sweep,
-  // bounded so the scratch stays well inside HBM.
-  const long cap = std::max<long>(65536, (long)(4096L * 1024L * 1024L / 8 / 200) / std::max(1, nlyr));
-  long target = std::min<long>(cap, 262144);
+long auto_chunk(long nsolve, int nn, int nlyr, bool planck) {
+  // Enough solves per chunk to fill 256 CUs (one lane per solve in the NN <= 8
+  // sweep, one 16-lane team per solve above), bounded so the scratch stays
+  // within a fixed HBM budget (the rest of the 288 GB stays the caller's).
+  const double budget = 8.0 * 1024.0 * 1024.0 * 1024.0;  // bytes of scratch per chunk
+  const double per = 8.0 * (double)hd::scratch_doubles_per_solve(nn, nlyr, planck);
+  const long floor_n = nn <= hd::kMaxRegNN ? 65536 : 16384;
+  const long cap = std::max<long>(floor_n, (long)(budget / per));
+  const long target = std::min<long>(cap, 262144);
   if (nsolve <= target) return nsolve;
   long n = (nsolve + target - 1) / target;
   return (nsolve + n - 1) / n;
@@ -271,7 +276,9 @@ int hd_context_reserve(hd_context* ctx, const hd_config* cfg, long nsolve) {
   if (cfg->nstr < 2 || cfg->nstr % 2 || cfg->nstr / 2 > hd::kMaxNN || cfg->nlyr < 1)
     return fail(ctx, HD_EINVAL, "hd_context_reserve: bad config");
   HD_HIP(ctx, hipSetDevice(ctx->device));
-  const long chunk = ctx->chunk > 0 ? std::min(ctx->chunk, nsolve) : auto_chunk(nsolve, cfg->nlyr);
+  const bool planck_r = (cfg->flags & HD_FLAG_PLANCK) != 0;
+  const long chunk = ctx->chunk > 0 ? std::min(ctx->chunk, nsolve)
+                                    : auto_chunk(nsolve, cfg->nstr / 2, cfg->nlyr, planck_r);
   const size_t per = hd::scratch_doubles_per_solve(cfg->nstr / 2, cfg->nlyr,
                                                    (cfg->flags & HD_FLAG_PLANCK) != 0);
   int rc = ensure_scratch(ctx, per * std::max<long>(chunk, 1));
@@ -302,9 +309,9 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
   const bool planck = (cfg->flags & HD_FLAG_PLANCK) != 0;
   const bool sync = status == nullptr;
 
-  long chunk = ctx->chunk > 0 ? std::min(ctx->chunk, nsolve) : auto_chunk(nsolve, nlyr);
-  const size_t ne1 = (size_t)(nn * (nn + 1) + 2 * nn + 1);
-  const size_t ne2 = (size_t)(nn * nn + 2 * nn + 1);
+  long chunk = ctx->chunk > 0 ? std::min(ctx->chunk, nsolve) : auto_chunk(nsolve, nn, nlyr, planck);
+  const size_t ne1 = hd::layer_record_doubles(nn);
+  const size_t ne2 = hd::bsub_record_doubles(nn);
   const size_t per = hd::scratch_doubles_per_solve(nn, nlyr, planck);
   rc = ensure_scratch(ctx, per * chunk);
   if (rc) return rc;
@@ -394,8 +401,11 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
       ctx->pool_used += 3;
     }
     const bool beam = in->fbeam != nullptr;
-    hipError_t e = hd::launch_solve_chunk_nn(nn, planck ? &pa : nullptr, beam ? &ta : nullptr, la,
-                                             sa, stream, ev);
+    hipError_t e = nn <= hd::kMaxRegNN
+                       ? hd::launch_solve_chunk_nn(nn, planck ? &pa : nullptr,
+                                                   beam ? &ta : nullptr, la, sa, stream, ev)
+                       : hd::launch_solve_chunk_team(nn, planck ? &pa : nullptr,
+                                                     beam ? &ta : nullptr, la, sa, stream, ev);
     if (e != hipSuccess) return fail(ctx, HD_EHIP, "hd_solve: launch failed: %s", hipGetErrorString(e));
   }
   if (sync) {

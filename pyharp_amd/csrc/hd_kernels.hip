@@ -781,9 +781,7 @@ hipError_t upload_quad_tables(const QuadHost* per_nn /* [kMaxNN], index nn-1 */)
   return hipMemcpyToSymbol(HIP_SYMBOL(c_quad), &t, sizeof(t), 0, hipMemcpyHostToDevice);
 }
 
-template <int NN>
-static hipError_t launch_chunk(const PlanckArgs* pa, const TaucArgs* ta, const LayerArgs& la,
-                               const SweepArgs& sa, hipStream_t stream, hipEvent_t* ev) {
+void launch_prologue(const PlanckArgs* pa, const TaucArgs* ta, hipStream_t stream) {
   if (ta) {
     hipLaunchKernelGGL(hd_tauc_kernel, dim3((unsigned)((ta->nsc + 255) / 256)), dim3(256), 0,
                        stream, *ta);
@@ -793,6 +791,12 @@ static hipError_t launch_chunk(const PlanckArgs* pa, const TaucArgs* ta, const L
     hipLaunchKernelGGL(hd_planck_kernel, dim3((unsigned)((n0 + 255) / 256)), dim3(256), 0,
                        stream, *pa);
   }
+}
+
+template <int NN>
+static hipError_t launch_chunk(const PlanckArgs* pa, const TaucArgs* ta, const LayerArgs& la,
+                               const SweepArgs& sa, hipStream_t stream, hipEvent_t* ev) {
+  launch_prologue(pa, ta, stream);
   const unsigned nb1 = (unsigned)(((la.nsc + 63) / 64) *
                                   ((la.nlyr + kLayersPerBlock - 1) / kLayersPerBlock));
   const unsigned nb2 = (unsigned)((la.nsc + 63) / 64);
@@ -820,10 +824,19 @@ hipError_t launch_solve_chunk_nn(int nn, const PlanckArgs* pa, const TaucArgs* t
   }
 }
 
+size_t layer_record_doubles(int nn) {
+  if (nn <= kMaxRegNN) return (size_t)(nn * (nn + 1) + 2 * nn + 1);
+  return (size_t)(2 * nn * nn + 2 * nn + 2);  // team layout: full R, T rows (+ pad to even)
+}
+
+size_t bsub_record_doubles(int nn) {
+  if (nn <= kMaxRegNN) return (size_t)(nn * nn + 2 * nn + 1);
+  return (size_t)((nn * nn + 2 * nn + 2) & ~1);
+}
+
 size_t scratch_doubles_per_solve(int nn, int nlyr, bool planck) {
-  const size_t ne1 = (size_t)(nn * (nn + 1) + 2 * nn + 1);
-  const size_t ne2 = (size_t)(nn * nn + 2 * nn + 1);
-  return (ne1 + ne2) * nlyr + (planck ? (size_t)nlyr + 3 : 0) + (size_t)nlyr;  // + tauc
+  return (layer_record_doubles(nn) + bsub_record_doubles(nn)) * nlyr +
+         (planck ? (size_t)nlyr + 3 : 0) + (size_t)nlyr;  // + tauc
 }
 
 }  // namespace hd

@@ -7,7 +7,9 @@
 
 namespace hd {
 
-constexpr int kMaxNN = 8;  // nstr <= 16 in this release
+constexpr int kMaxNN = 16;    // nstr <= 32
+constexpr int kMaxRegNN = 8;  // one-lane-per-problem kernels (hd_kernels.hip) up to nstr 16;
+                              // 16-lane team kernels (hd_team.hip) for nstr 18..32
 
 template <int NN>
 __host__ __device__ constexpr int ne1() {  // per-layer operator record (doubles)
@@ -91,11 +93,20 @@ struct QuadHost {
 };
 
 // copy the quadrature tables (index nn-1) into the current device's constant memory
-hipError_t upload_quad_tables(const QuadHost* per_nn);
+hipError_t upload_quad_tables(const QuadHost* per_nn);       // nn 1..kMaxRegNN
+hipError_t upload_quad_tables_team(const QuadHost* per_nn);  // nn kMaxRegNN+1..kMaxNN
+// cumulative scaled depth (beam) and level Planck radiances (planck) of a chunk
+void launch_prologue(const PlanckArgs* pa, const TaucArgs* ta, hipStream_t stream);
 // ev: 3 events (before K1, between, after K2) or nullptr; pa null when planck is off
 hipError_t launch_solve_chunk_nn(int nn, const PlanckArgs* pa, const TaucArgs* ta,
                                  const LayerArgs& la, const SweepArgs& sa, hipStream_t stream,
                                  hipEvent_t* ev);
+hipError_t launch_solve_chunk_team(int nn, const PlanckArgs* pa, const TaucArgs* ta,
+                                   const LayerArgs& la, const SweepArgs& sa, hipStream_t stream,
+                                   hipEvent_t* ev);
 size_t scratch_doubles_per_solve(int nn, int nlyr, bool planck);
+// doubles per (layer, solve) of the layer-operator and back-substitution records
+size_t layer_record_doubles(int nn);
+size_t bsub_record_doubles(int nn);
 
 }  // namespace hd

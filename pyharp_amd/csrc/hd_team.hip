@@ -1,0 +1,864 @@
+// hd_team.hip -- gfx950 kernels of the flux-only discrete-ordinate solve for
+// nstr 18..32 (NN = nstr/2 in 9..16), where one problem's NN x NN matrices no
+// longer fit one lane's registers.
+//
+//   hd_team_layer_kernel<NN>  one 16-lane team per (solve, layer): the same
+//                             per-layer setup as hd_layer_kernel (delta-M,
+//                             phase-matrix assembly, Cholesky + Jacobi
+//                             symmetric eigenproblem, beam/thermal particular
+//                             solutions, R~/T~/S~ in the flux-weighted basis;
+//                             DESIGN.md section 3)        [c_setdis, c_soleig,
+//                             c_upbeam, c_upisot]
+//   hd_team_sweep_kernel<NN>  one team per solve: adding sweep top->bottom,
+//                             Lambertian surface, back-substitution, level
+//                             fluxes in harp layout     [c_setmtx, c_solve0,
+//                             c_fluxes]
+//
+// Team layout: a team is one DPP row (16 lanes of a wave64); lane i owns row i
+// of every NN x NN matrix and element i of every vector (lanes i >= NN carry
+// zeros).  All cross-lane traffic is DPP inside the row -- row_newbcast:k
+// (one v_mov_b64_dpp) hands lane k's value to the whole team, row_ror and the
+// quad/half/full mirrors give the XOR permutations of the parallel Jacobi
+// ordering and the team sums.  No LDS, no barriers: a team is always wholly
+// active or wholly inactive, so every DPP source lane is live.
+//
+// Scratch records, solve-major inside a layer (a team's record is contiguous):
+//   layer ops [lc][s][2NN^2+2NN+2]  R~ rows | T~ rows | S~+ | S~- | tau' | pad
+//   back-sub  [lc][s][NN^2+2NN+1 -> even]  ZT rows | t | rc | cs | pad
+#include <utility>
+
+#include "hd_kernels.hpp"
+
+namespace hd {
+
+struct QuadTablesTeam {
+  Quad<9> q9;
+  Quad<10> q10;
+  Quad<11> q11;
+  Quad<12> q12;
+  Quad<13> q13;
+  Quad<14> q14;
+  Quad<15> q15;
+  Quad<16> q16;
+};
+__constant__ QuadTablesTeam c_quad_team;
+
+template <int NN>
+__device__ __forceinline__ const Quad<NN>& tquad() {
+  if constexpr (NN == 9) return c_quad_team.q9;
+  else if constexpr (NN == 10) return c_quad_team.q10;
+  else if constexpr (NN == 11) return c_quad_team.q11;
+  else if constexpr (NN == 12) return c_quad_team.q12;
+  else if constexpr (NN == 13) return c_quad_team.q13;
+  else if constexpr (NN == 14) return c_quad_team.q14;
+  else if constexpr (NN == 15) return c_quad_team.q15;
+  else return c_quad_team.q16;
+}
+
+namespace {
+
+constexpr int kTeam = 16;
+constexpr int kTeamBlock = 256;
+constexpr int kTeamsPerBlock = kTeamBlock / kTeam;
+
+// ---- compile-time loops (DPP controls must be immediates) -------------------
+template <int B, class F, int... Is>
+__device__ __forceinline__ void sfor_impl(F&& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, B + Is>{}), ...);
+}
+// f(k) for k = B .. E-1 (ascending)
+template <int B, int E, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (E > B) sfor_impl<B>(f, std::make_integer_sequence<int, E - B>{});
+}
+template <int B, class F, int... Is>
+__device__ __forceinline__ void sfor_rev_impl(F&& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, B - Is>{}), ...);
+}
+// f(k) for k = E-1 .. B (descending)
+template <int B, int E, class F>
+__device__ __forceinline__ void sfor_rev(F&& f) {
+  if constexpr (E > B) sfor_rev_impl<E - 1>(f, std::make_integer_sequence<int, E - B>{});
+}
+#define HD_K(x) decltype(x)::value
+
+// ---- DPP primitives ----------------------------------------------------------
+__device__ __forceinline__ int tlane() { return (int)(threadIdx.x & (kTeam - 1)); }
+
+template <int CTRL>
+__device__ __forceinline__ double dpp(double x) {
+  return __builtin_amdgcn_update_dpp(0.0, x, CTRL, 0xF, 0xF, false);
+}
+// value held by team lane K (row_newbcast:K)
+template <int K>
+__device__ __forceinline__ double bc(double x) {
+  return dpp<0x150 + K>(x);
+}
+constexpr int quad_xor(int m) {
+  return (0 ^ m) | ((1 ^ m) << 2) | ((2 ^ m) << 4) | ((3 ^ m) << 6);
+}
+// value held by team lane (i ^ M): XOR masks compose, so M = hi ^ lo is built
+// from row_half_mirror (^7), row_ror:8 (^8), row_mirror (^15) and a quad_perm
+template <int M>
+__device__ __forceinline__ double xperm(double x) {
+  static_assert(M > 0 && M < 16, "team XOR mask");
+  constexpr int hi = M & 12;
+  constexpr int lo = (hi == 4 || hi == 12) ? ((M & 3) ^ 3) : (M & 3);
+  if constexpr (hi == 4) x = dpp<0x141>(x);
+  else if constexpr (hi == 8) x = dpp<0x128>(x);
+  else if constexpr (hi == 12) x = dpp<0x140>(x);
+  if constexpr (lo != 0) x = dpp<quad_xor(lo)>(x);
+  return x;
+}
+// sum over the 16 lanes of the team (every lane receives a sum; the
+// association differs per lane, so take bc<0>() where a uniform value matters)
+__device__ __forceinline__ double team_sum(double x) {
+  x += dpp<0x128>(x);
+  x += dpp<0x124>(x);
+  x += dpp<0x122>(x);
+  x += dpp<0x121>(x);
+  return x;
+}
+
+// ---- team linear algebra (lane i = row i) ------------------------------------
+
+// Cholesky of the SPD matrix whose row i lane i holds in a.  Out: a = row i of
+// L (zeros above the diagonal); lt = row i of L^T (column i of L) if WANT_LT;
+// rd = 1/L_ii.  Returns false on a non-positive pivot (uniform over the team).
+template <int NN, bool WANT_LT>
+__device__ __forceinline__ bool team_chol(double (&a)[NN], double (&lt)[NN], double& rd) {
+  const int i = tlane();
+  bool ok = true;
+  rd = 0.0;
+  if constexpr (WANT_LT) sfor<0, NN>([&](auto J) { lt[HD_K(J)] = 0.0; });
+  sfor<0, NN>([&](auto K) {
+    constexpr int k = HD_K(K);
+    double d = bc<k>(a[k]);
+    ok = ok && d > 0.0;
+    d = d > 1.0e-300 ? d : 1.0e-300;
+    const double r = rsq_nr(d);
+    const double lkk = d * r;
+    const double aik = a[k] * r;
+    a[k] = i > k ? aik : (i == k ? lkk : 0.0);
+    if (i == k) rd = r;
+    if constexpr (WANT_LT) {
+      if (i == k) lt[k] = lkk;
+    }
+    sfor<k + 1, NN>([&](auto J) {
+      constexpr int j = HD_K(J);
+      const double ljk = bc<j>(a[k]);
+      a[j] = fma(-a[k], ljk, a[j]);  // above the diagonal: zeroed at step j
+      if constexpr (WANT_LT) {
+        if (i == k) lt[j] = ljk;
+      }
+    });
+  });
+  return ok;
+}
+
+// x <- L^-1 x  (x distributed: lane i holds x_i)
+template <int NN>
+__device__ __forceinline__ void team_lsolve(const double (&l)[NN], double rd, double& x) {
+  const int i = tlane();
+  sfor<0, NN>([&](auto K) {
+    constexpr int k = HD_K(K);
+    if (i == k) x *= rd;
+    const double xk = bc<k>(x);
+    if (i > k) x = fma(-l[k], xk, x);
+  });
+}
+
+// x <- L^-T x  (lt = rows of L^T)
+template <int NN>
+__device__ __forceinline__ void team_usolve(const double (&lt)[NN], double rd, double& x) {
+  const int i = tlane();
+  sfor_rev<0, NN>([&](auto K) {
+    constexpr int k = HD_K(K);
+    if (i == k) x *= rd;
+    const double xk = bc<k>(x);
+    if (i < k) x = fma(-lt[k], xk, x);
+  });
+}
+
+// X <- L^-T X  (X rows distributed)
+template <int NN>
+__device__ __forceinline__ void team_umsolve(const double (&lt)[NN], double rd, double (&x)[NN]) {
+  const int i = tlane();
+  sfor_rev<0, NN>([&](auto K) {
+    constexpr int k = HD_K(K);
+    const double sc = i == k ? rd : 1.0;
+    sfor<0, NN>([&](auto J) { x[HD_K(J)] *= sc; });
+    const double m = i < k ? lt[k] : 0.0;
+    sfor<0, NN>([&](auto J) {
+      constexpr int j = HD_K(J);
+      x[j] = fma(-m, bc<k>(x[j]), x[j]);
+    });
+  });
+}
+
+// ---- Jacobi eigensolver, XOR parallel ordering --------------------------------
+// Round M pairs lane i with lane i^M; rounds 1..15 cover every pair once.
+template <int NN>
+__host__ __device__ constexpr bool round_has_pair(int m) {
+  for (int p = 0; p < NN; ++p)
+    if ((p ^ m) > p && (p ^ m) < NN) return true;
+  return false;
+}
+
+template <int NN, int M>
+__device__ __forceinline__ void team_jacobi_round(double (&a)[NN], double (&v)[NN], bool on) {
+  const int i = tlane();
+  double cc[NN], ss[NN];
+  double c_own = 1.0, s_own = 0.0;  // this lane's pair; s carries the side's sign
+  sfor<0, NN>([&](auto P) {
+    constexpr int p = HD_K(P), q = p ^ M;
+    if constexpr (q > p && q < NN) {
+      // w = sqrt(d^2 + 4 a^2), u = |d| + w, z = 1/sqrt(2 w u): c = u z, s = sgn(d) 2 a z
+      const double app = bc<p>(a[p]), aqq = bc<q>(a[q]), apq = bc<p>(a[q]);
+      const double d = aqq - app;
+      const double w2 = fma(d, d, 4.0 * apq * apq);
+      const bool rot = on && w2 > 1.0e-280;
+      const double w2s = rot ? w2 : 1.0;
+      const double w = w2s * rsq_nr(w2s);
+      const double u = fabs(d) + w;
+      const double z = rsq_nr(2.0 * w * u);
+      const double sg = d < 0.0 ? -2.0 : 2.0;
+      const double c = rot ? u * z : 1.0;
+      const double s = rot ? sg * apq * z : 0.0;
+      cc[p] = c;
+      ss[p] = s;
+      if (i == p || i == q) c_own = c;
+      if (i == p) s_own = -s;
+      if (i == q) s_own = s;
+    }
+  });
+  // B = A J, V <- V J (column rotations: lane-local)
+  sfor<0, NN>([&](auto P) {
+    constexpr int p = HD_K(P), q = p ^ M;
+    if constexpr (q > p && q < NN) {
+      const double c = cc[p], s = ss[p];
+      const double ap = a[p], aq = a[q];
+      a[p] = fma(c, ap, -s * aq);
+      a[q] = fma(s, ap, c * aq);
+      const double vp = v[p], vq = v[q];
+      v[p] = fma(c, vp, -s * vq);
+      v[q] = fma(s, vp, c * vq);
+    }
+  });
+  // A' = J^T B: row p' = c b_p - s b_q, row q' = s b_p + c b_q (partner = lane i^M)
+  sfor<0, NN>([&](auto J) {
+    constexpr int j = HD_K(J);
+    const double b = xperm<M>(a[j]);
+    a[j] = fma(s_own, b, c_own * a[j]);
+  });
+  if (on) {  // the rotated pairs are zero by construction
+    sfor<0, NN>([&](auto P) {
+      constexpr int p = HD_K(P), q = p ^ M;
+      if constexpr (q > p && q < NN) {
+        if (i == p) a[q] = 0.0;
+        if (i == q) a[p] = 0.0;
+      }
+    });
+  }
+}
+
+// a (rows of a symmetric matrix) -> eigenvalues on the diagonal, eigenvectors
+// in the columns of v (rows distributed).  A converged team stops rotating;
+// the loop ends when every team of the wave has converged or after max_sweeps.
+template <int NN>
+__device__ __forceinline__ void team_jacobi(double (&a)[NN], double (&v)[NN], int max_sweeps) {
+  const int i = tlane();
+  sfor<0, NN>([&](auto J) { v[HD_K(J)] = i == HD_K(J) ? 1.0 : 0.0; });
+  for (int sweep = 0; sweep < max_sweeps; ++sweep) {
+    double off = 0.0, dia = 0.0;
+    sfor<0, NN>([&](auto J) {
+      constexpr int j = HD_K(J);
+      const double x2 = a[j] * a[j];
+      if (i == j) dia += x2;
+      else off += x2;
+    });
+    off = bc<0>(team_sum(off));
+    dia = bc<0>(team_sum(dia));
+    const bool done = !(off > 2.0e-30 * dia);  // both triangles: the 1e-30 of jacobi_eig
+    if (__all(done)) break;
+    sfor<1, kTeam>([&](auto Mc) {
+      constexpr int m = HD_K(Mc);
+      if constexpr (round_has_pair<NN>(m)) team_jacobi_round<NN, m>(a, v, !done);
+    });
+  }
+}
+
+}  // namespace
+
+template <int NN>
+constexpr int ne1t() {
+  return 2 * NN * NN + 2 * NN + 2;
+}
+template <int NN>
+constexpr int ne2t() {
+  return (NN * NN + 2 * NN + 2) & ~1;
+}
+
+// ============================================================================
+// K1 (team): per-(solve, layer) setup
+// ============================================================================
+template <int NN>
+__global__ __launch_bounds__(kTeamBlock) void hd_team_layer_kernel(LayerArgs A) {
+  constexpr int N = 2 * NN;
+  const Quad<NN>& Qc = tquad<NN>();
+  const int i = tlane();
+  const bool act = i < NN;
+  const int ii = act ? i : 0;
+  const long team = (long)blockIdx.x * kTeamsPerBlock + (threadIdx.x >> 4);
+  const int L = A.nlyr;
+  if (team >= (long)A.nsc * L) return;  // whole team
+  // consecutive teams = consecutive solves of one layer -> contiguous records
+  const int sl = (int)(team % A.nsc);
+  const int lc = (int)(team / A.nsc);
+  const long s = A.s0 + sl;
+  const int nm = A.nmom;
+  const int np = A.nprop;
+  int st = 0;
+
+  const double mu_i = act ? Qc.mu[ii] : 1.0;
+  const double sd_i = act ? Qc.sd[ii] : 0.0;
+  const double g_i = act ? Qc.g[ii] : 0.0;
+  const double rmu_i = act ? Qc.rmu[ii] : 0.0;
+  const double rg_i = act ? Qc.rg[ii] : 0.0;
+
+  // ---- inputs of this layer (harp layer L-1-lc) + delta-M (c_setdis) ----
+  const double* q = A.prop + ((size_t)s * L + (L - 1 - lc)) * np;
+  const double tau = q[0];
+  double ssa = np > 1 ? q[1] : 0.0;
+  if (!(tau >= 0.0) || !(ssa >= 0.0) || !(ssa <= 1.0)) st |= kStBadInput;
+  if (ssa == 1.0) ssa = 1.0 - kDither;
+  const double f = nm >= N ? q[1 + N] : 0.0;
+  if (!(f < 1.0)) st |= kStBadInput;
+  const double taup = (1.0 - ssa * f) * tau;
+  const double om = ssa * (1.0 - f) / (1.0 - ssa * f);
+  const double rf = om / (1.0 - f);
+
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
+  const double fb = A.fbeam ? A.fbeam[s] : 0.0;
+  const bool beam = fb > 0.0 && mu0 > 0.0;
+  if (beam && mu0 > 1.0) st |= kStBadInput;
+  const double rmu0 = beam ? 1.0 / mu0 : 0.0;
+  const double mub = beam ? mu0 : 0.0;
+
+  // ---- phase-matrix rows: -A+ (ap), -A- (lch); beam source elements ----
+  double ap[NN], lch[NN];
+  double xs = 0.0, xd = 0.0;
+  sfor<0, NN>([&](auto J) { ap[HD_K(J)] = lch[HD_K(J)] = 0.0; });
+  {
+    double pprev = 0.0, pcur = 1.0;
+#pragma nounroll
+    for (int l2 = 0; l2 < NN; ++l2) {
+      const int le = 2 * l2, lo = le + 1;
+      const double che = le == 0 ? 1.0 : (le <= nm ? q[1 + le] : 0.0);
+      const double cho = lo <= nm ? q[1 + lo] : 0.0;
+      const double ge = (2 * le + 1) * (che - f) * rf;
+      const double go = (2 * lo + 1) * (cho - f) * rf;
+      const double pe0 = pcur;
+      const double po0 = ((2 * lo - 1) * mub * pcur - (lo - 1) * pprev) / lo;
+      pprev = po0;
+      pcur = ((2 * lo + 1) * mub * po0 - lo * pe0) / (lo + 1);
+      const double ue = act ? ge * Qc.pt[le][ii] : 0.0;
+      const double uo = act ? go * Qc.pt[lo][ii] : 0.0;
+      xs = fma(ue, pe0, xs);
+      xd = fma(uo, po0, xd);
+      sfor<0, NN>([&](auto J) {
+        constexpr int j = HD_K(J);
+        ap[j] = fma(ue, Qc.pt[le][j], ap[j]);
+        lch[j] = fma(uo, Qc.pt[lo][j], lch[j]);
+      });
+    }
+  }
+  sfor<0, NN>([&](auto J) {
+    constexpr int j = HD_K(J);
+    const double diag = i == j ? rmu_i : 0.0;
+    const double sij = sd_i * Qc.sd[j];
+    lch[j] = fma(-sij, lch[j], diag);
+    ap[j] = fma(-sij, ap[j], diag);
+  });
+  // L L^T = -A-
+  double lt[NN], rdl;
+  if (!team_chol<NN, true>(lch, lt, rdl)) st |= kStEigen;
+
+  // ---- pre-Jacobi vectors (depend on L only) ----
+  double y2 = 0.0, lxd = 0.0;
+  const double fb2 = fb * (0.5 / kPi);
+  if (beam) {
+    const double y = sd_i * (fb2 * xs);
+    double z = 0.0;  // z = L^T y
+    sfor<0, NN>([&](auto K) { z = fma(lt[HD_K(K)], bc<HD_K(K)>(y), z); });
+    double yl = 0.0;  // L z
+    sfor<0, NN>([&](auto K) { yl = fma(lch[HD_K(K)], bc<HD_K(K)>(z), yl); });
+    const double xdi = -fb2 * xd;
+    const double rv = fma(-yl, rg_i, xdi * rmu0 * rmu_i);
+    y2 = g_i * rv;
+    lxd = sd_i * xdi;
+    team_lsolve<NN>(lch, rdl, y2);
+    team_lsolve<NN>(lch, rdl, lxd);
+    team_usolve<NN>(lt, rdl, lxd);
+  }
+  double cvec = 0.0, db = 0.0, bsum = 0.0;
+  if (A.planck) {
+    const double bt = A.planckv[(size_t)(L - lc) * A.nsc + sl];
+    const double bb = A.planckv[(size_t)(L - lc - 1) * A.nsc + sl];
+    db = bb - bt;
+    bsum = bt + bb;
+    const double b1 = taup > 0.0 ? 2.0 * db / taup : 0.0;
+    cvec = sd_i * mu_i;
+    team_lsolve<NN>(lch, rdl, cvec);
+    team_usolve<NN>(lt, rdl, cvec);
+    cvec = act ? fma(b1 * rg_i, cvec, db) : 0.0;
+  }
+
+  // ---- Sym = L^T (-A+) L ----
+  double sym[NN];
+  {
+    double m[NN];
+    sfor<0, NN>([&](auto J) {
+      constexpr int j = HD_K(J);
+      double t = 0.0;
+      sfor<j, NN>([&](auto K) { t = fma(ap[HD_K(K)], bc<HD_K(K)>(lch[j]), t); });
+      m[j] = t;
+    });
+    sfor<0, NN>([&](auto J) {
+      constexpr int j = HD_K(J);
+      double t = 0.0;
+      sfor<0, NN>([&](auto K) { t = fma(lt[HD_K(K)], bc<HD_K(K)>(m[j]), t); });
+      sym[j] = t;
+    });
+  }
+
+  // ---- eigenpairs (c_soleig): Sym = V diag(k^2) V^T ----
+  double v[NN];
+  team_jacobi<NN>(sym, v, A.max_sweeps);
+  double k2 = 0.0;
+  sfor<0, NN>([&](auto J) {
+    if (i == HD_K(J)) k2 = sym[HD_K(J)];
+  });
+  if (act && !(k2 > 0.0)) st |= kStEigen;
+  const double kk = sqrt(k2 > 0.0 ? k2 : 0.0);  // lane j: eigenvalue of column j
+  // vt = V^T rows (lane j: column j of V)
+  double vt[NN];
+  sfor<0, NN>([&](auto Ai) {
+    constexpr int a = HD_K(Ai);
+    vt[a] = 0.0;
+    sfor<0, NN>([&](auto J) {
+      const double x = bc<a>(v[HD_K(J)]);
+      if (i == HD_K(J)) vt[a] = x;
+    });
+  });
+
+  // ---- beam particular solution Z+/- (c_upbeam) ----
+  double zp = 0.0, zm = 0.0, e0 = 0.0;
+  if (beam) {
+    const double r2 = rmu0 * rmu0;
+    double t = 0.0;  // (V^T y2)_j
+    sfor<0, NN>([&](auto K) { t = fma(vt[HD_K(K)], bc<HD_K(K)>(y2), t); });
+    double den = fma(-kk, kk, r2);
+    if (act && fabs(den) < 1.0e-9 * r2) {
+      st |= kStResonance;
+      den = den < 0.0 ? -1.0e-9 * r2 : 1.0e-9 * r2;
+    }
+    const double tt = act ? t / den : 0.0;
+    double y = 0.0;  // V tt
+    sfor<0, NN>([&](auto J) { y = fma(v[HD_K(J)], bc<HD_K(J)>(tt), y); });
+    double sv = 0.0;  // W^-1 D^1/2 L y
+    sfor<0, NN>([&](auto K) { sv = fma(lch[HD_K(K)], bc<HD_K(K)>(y), sv); });
+    sv *= rg_i;
+    double yy = sd_i * mu_i * sv;
+    team_lsolve<NN>(lch, rdl, yy);
+    team_usolve<NN>(lt, rdl, yy);
+    const double tauc = A.tauc[(size_t)lc * A.nsc + sl];
+    const double att = 0.5 * exp(-tauc * rmu0);
+    const double dd = rg_i * fma(-yy, rmu0, lxd);
+    zp = (sv + dd) * att;
+    zm = (sv - dd) * att;
+    e0 = exp(-taup * rmu0);
+  }
+
+  // ---- layer operators in the flux-weighted basis ----
+  double dsq, gsq;
+  {
+    const double x = kk * taup;
+    const double m = -expm1(-x);
+    const double th = m * rcp_nr(2.0 - m);
+    const double delta = x > 1.0e-8 ? th * rcp_nr(kk > 0.0 ? kk : 1.0) : 0.5 * taup;
+    dsq = sqrt(delta);
+    gsq = sqrt(kk * th);
+  }
+  // Psi^T rows = L^-T V Gamma^1/2
+  double pst[NN];
+  sfor<0, NN>([&](auto J) { pst[HD_K(J)] = v[HD_K(J)] * bc<HD_K(J)>(gsq); });
+  team_umsolve<NN>(lt, rdl, pst);
+  // Omega rows = L V Delta^1/2
+  double omr[NN];
+  sfor<0, NN>([&](auto J) {
+    constexpr int j = HD_K(J);
+    double t = 0.0;
+    sfor<0, NN>([&](auto K) { t = fma(lch[HD_K(K)], bc<HD_K(K)>(v[j]), t); });
+    omr[j] = t * bc<j>(dsq);
+  });
+  // Omega^T rows (lane j): dsq_j sum_a V_aj L_ca
+  double omt[NN];
+  sfor<0, NN>([&](auto C) {
+    constexpr int c = HD_K(C);
+    double t = 0.0;
+    sfor<0, c + 1>([&](auto K) { t = fma(vt[HD_K(K)], bc<c>(lch[HD_K(K)]), t); });
+    omt[c] = t * dsq;
+  });
+  // Psi rows (lane j): gsq_j (V^T)_j L^-1, i.e. x L = vt_j by backward columns
+  double psr[NN];
+  sfor_rev<0, NN>([&](auto C) {
+    constexpr int c = HD_K(C);
+    double t = vt[c];
+    sfor<c + 1, NN>([&](auto K) { t = fma(-psr[HD_K(K)], bc<HD_K(K)>(lch[c]), t); });
+    psr[c] = t * bc<c>(rdl);
+  });
+  sfor<0, NN>([&](auto J) { psr[HD_K(J)] *= gsq; });
+
+  const double ga = g_i * (cvec - fma(-zp, e0, zm));
+  const double gb = g_i * (fma(zp, e0, zm) + bsum);
+  // Q~- = Phi Phi^T, Phi = Omega J^-T, J J^T = I + Omega^T Omega
+  double qm[NN], pv = 0.0;
+  {
+    double hm[NN];
+    sfor<0, NN>([&](auto J) {
+      constexpr int j = HD_K(J);
+      double t = i == j ? 1.0 : 0.0;
+      sfor<0, NN>([&](auto K) { t = fma(omt[HD_K(K)], bc<HD_K(K)>(omr[j]), t); });
+      hm[j] = t;
+    });
+    double unused[NN], jrd;
+    if (!team_chol<NN, false>(hm, unused, jrd)) st |= kStEigen;
+    double ph[NN];
+    sfor<0, NN>([&](auto J) {
+      constexpr int j = HD_K(J);
+      double t = omr[j];
+      sfor<0, j>([&](auto K) { t = fma(-bc<j>(hm[HD_K(K)]), ph[HD_K(K)], t); });
+      ph[j] = t * bc<j>(jrd);
+    });
+    sfor<0, NN>([&](auto J) {
+      constexpr int j = HD_K(J);
+      double t = 0.0;
+      sfor<0, NN>([&](auto K) { t = fma(ph[HD_K(K)], bc<j>(ph[HD_K(K)]), t); });
+      qm[j] = t;
+      pv = fma(t, bc<j>(ga), pv);
+    });
+  }
+  // Q~+ = -Xi^T Xi, Xi^T rows = Psi^T rows through J+, J+ J+^T = I + Psi Psi^T
+  double qp[NN], qv = 0.0;
+  {
+    double hp[NN];
+    sfor<0, NN>([&](auto J) {
+      constexpr int j = HD_K(J);
+      double t = i == j ? 1.0 : 0.0;
+      sfor<0, NN>([&](auto K) { t = fma(psr[HD_K(K)], bc<j>(psr[HD_K(K)]), t); });
+      hp[j] = t;
+    });
+    double unused[NN], jrd;
+    if (!team_chol<NN, false>(hp, unused, jrd)) st |= kStEigen;
+    double xi[NN];
+    sfor<0, NN>([&](auto J) {
+      constexpr int j = HD_K(J);
+      double t = pst[j];
+      sfor<0, j>([&](auto K) { t = fma(-bc<j>(hp[HD_K(K)]), xi[HD_K(K)], t); });
+      xi[j] = t * bc<j>(jrd);
+    });
+    sfor<0, NN>([&](auto J) {
+      constexpr int j = HD_K(J);
+      double t = 0.0;
+      sfor<0, NN>([&](auto K) { t = fma(xi[HD_K(K)], bc<j>(xi[HD_K(K)]), t); });
+      qp[j] = -t;
+      qv = fma(-t, bc<j>(gb), qv);
+    });
+  }
+
+  // ---- store: R~ = Q~- + Q~+, T~ = I - Q~- + Q~+ (rows), S~+, S~-, tau' ----
+  double* out = A.scr + ((size_t)lc * A.nsc + sl) * ne1t<NN>();
+  double chk = 0.0;
+  if (act) {
+    sfor<0, NN>([&](auto J) {
+      constexpr int j = HD_K(J);
+      const double r = qm[j] + qp[j];
+      const double t = (i == j ? 1.0 : 0.0) - qm[j] + qp[j];
+      out[i * NN + j] = r;
+      out[NN * NN + i * NN + j] = t;
+      chk += r + t;
+    });
+    const double sp = g_i * (zp * (1.0 - e0) - db) + pv - qv;
+    const double sm = g_i * (-zm * (1.0 - e0) + db) - pv - qv;
+    out[2 * NN * NN + i] = sp;
+    out[2 * NN * NN + NN + i] = sm;
+    chk += sp + sm;
+  }
+  if (i == 0) out[2 * NN * NN + 2 * NN] = taup;
+  if (!isfinite(chk + taup)) st |= kStNonFinite;
+  if (st) {
+    atomicOr(&A.status[s], st);
+    if (st & 0x0F) atomicOr(A.anyerr, 1);
+  }
+}
+
+// ============================================================================
+// K2 (team): per-solve adding sweep + back-substitution
+// ============================================================================
+template <int NN>
+__global__ __launch_bounds__(kTeamBlock) void hd_team_sweep_kernel(SweepArgs A) {
+  const Quad<NN>& Qc = tquad<NN>();
+  const int i = tlane();
+  const bool act = i < NN;
+  const int ii = act ? i : 0;
+  const long team = (long)blockIdx.x * kTeamsPerBlock + (threadIdx.x >> 4);
+  if (team >= A.nsc) return;  // whole team
+  const int sl = (int)team;
+  const long s = A.s0 + sl;
+  const int L = A.nlyr;
+  const size_t nsc = A.nsc;
+  int st = 0;
+  const double g_i = act ? Qc.g[ii] : 0.0;
+
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
+  const double fb = A.fbeam ? A.fbeam[s] : 0.0;
+  const bool beam = fb > 0.0 && mu0 > 0.0;
+  const double alb = A.albedo ? A.albedo[s] : 0.0;
+  if (!(alb >= 0.0) || !(alb <= 1.0)) st |= kStBadInput;
+  double top = A.fisot ? A.fisot[s] : 0.0;
+  double bsurf = 0.0;
+  if (A.planck) {
+    bsurf = A.planckv[(size_t)(L + 1) * nsc + sl];
+    top += A.planckv[(size_t)(L + 2) * nsc + sl];
+  }
+  const double twopi = 2.0 * kPi;
+  const double rmu0 = beam ? 1.0 / mu0 : 0.0;
+  const double f0mu0 = beam ? fb * mu0 : 0.0;
+
+  double ra[NN];  // reflection of the stack above (row i)
+  double sd = g_i * top;  // diffuse downward source at the current interface
+  sfor<0, NN>([&](auto J) { ra[HD_K(J)] = 0.0; });
+  double tauc = 0.0;
+
+  for (int lc = 0; lc < L; ++lc) {
+    const double* rec = A.scr + ((size_t)lc * nsc + sl) * ne1t<NN>();
+    double* bp = A.bsub + ((size_t)lc * nsc + sl) * ne2t<NN>();
+    double rl[NN];
+    sfor<0, NN>([&](auto J) { rl[HD_K(J)] = act ? rec[ii * NN + HD_K(J)] : 0.0; });
+    const double spl = act ? rec[2 * NN * NN + ii] : 0.0;
+    const double sml = act ? rec[2 * NN * NN + NN + ii] : 0.0;
+
+    // level lc (top of layer lc): F_dn = rc . I+ + cs
+    {
+      double t = 0.0;
+      sfor<0, NN>([&](auto J) { t = fma(ra[HD_K(J)], Qc.g[HD_K(J)], t); });
+      if (act) bp[NN * NN + NN + i] = twopi * t;
+      const double cs = team_sum(g_i * sd);
+      if (i == 0) bp[NN * NN + 2 * NN] = fma(twopi, cs, f0mu0 * exp(-tauc * rmu0));
+    }
+    // W1 = I - R_l A ; t1 = R_l Sd + S+
+    double w[NN];
+    sfor<0, NN>([&](auto J) {
+      constexpr int j = HD_K(J);
+      double t = i == j ? 1.0 : 0.0;
+      sfor<0, NN>([&](auto K) { t = fma(-rl[HD_K(K)], bc<HD_K(K)>(ra[j]), t); });
+      w[j] = t;
+    });
+    double t1 = spl;
+    sfor<0, NN>([&](auto K) { t1 = fma(rl[HD_K(K)], bc<HD_K(K)>(sd), t1); });
+    // LU without pivoting; reciprocal pivots on the diagonal
+    sfor<0, NN>([&](auto K) {
+      constexpr int k = HD_K(K);
+      const double piv = bc<k>(w[k]);
+      if (!(fabs(piv) > 1.0e-12)) st |= kStPivot;
+      const double rp = rcp_nr(piv);
+      const double lik = w[k] * rp;
+      const double m = i > k ? lik : 0.0;
+      w[k] = i == k ? rp : (i > k ? lik : w[k]);
+      sfor<k + 1, NN>([&](auto J) {
+        constexpr int j = HD_K(J);
+        w[j] = fma(-m, bc<k>(w[j]), w[j]);
+      });
+    });
+    // t1 <- W1^-1 t1
+    sfor<0, NN>([&](auto K) {
+      constexpr int k = HD_K(K);
+      const double tk = bc<k>(t1);
+      if (i > k) t1 = fma(-w[k], tk, t1);
+    });
+    sfor_rev<0, NN>([&](auto K) {
+      constexpr int k = HD_K(K);
+      if (i == k) t1 *= w[k];
+      const double tk = bc<k>(t1);
+      if (i < k) t1 = fma(-w[k], tk, t1);
+    });
+    // u = A t1 + Sd
+    double u = sd;
+    sfor<0, NN>([&](auto K) { u = fma(ra[HD_K(K)], bc<HD_K(K)>(t1), u); });
+    if (act) bp[NN * NN + i] = t1;
+    // M1 = A W1^-1 (row-local): z U = a, then x L = z
+    double am[NN];
+    sfor<0, NN>([&](auto J) {
+      constexpr int j = HD_K(J);
+      double t = ra[j];
+      sfor<0, j>([&](auto K) { t = fma(-am[HD_K(K)], bc<HD_K(K)>(w[j]), t); });
+      am[j] = t * bc<j>(w[j]);
+    });
+    sfor_rev<0, NN>([&](auto J) {
+      constexpr int j = HD_K(J);
+      double t = am[j];
+      sfor<j + 1, NN>([&](auto K) { t = fma(-am[HD_K(K)], bc<HD_K(K)>(w[j]), t); });
+      am[j] = t;
+    });
+    // T~ rows; ZT = W1^-1 T (row-sequential solves)
+    double tr[NN], zt[NN];
+    sfor<0, NN>([&](auto J) {
+      constexpr int j = HD_K(J);
+      tr[j] = act ? rec[NN * NN + ii * NN + j] : 0.0;
+      zt[j] = tr[j];
+    });
+    sfor<0, NN>([&](auto K) {
+      constexpr int k = HD_K(K);
+      const double m = i > k ? w[k] : 0.0;
+      sfor<0, NN>([&](auto J) { zt[HD_K(J)] = fma(-m, bc<k>(zt[HD_K(J)]), zt[HD_K(J)]); });
+    });
+    sfor_rev<0, NN>([&](auto K) {
+      constexpr int k = HD_K(K);
+      const double sc = i == k ? w[k] : 1.0;
+      sfor<0, NN>([&](auto J) { zt[HD_K(J)] *= sc; });
+      const double m = i < k ? w[k] : 0.0;
+      sfor<0, NN>([&](auto J) { zt[HD_K(J)] = fma(-m, bc<k>(zt[HD_K(J)]), zt[HD_K(J)]); });
+    });
+    if (act) sfor<0, NN>([&](auto J) { bp[i * NN + HD_K(J)] = zt[HD_K(J)]; });
+    // P = M1 T ; Ra <- R_l + T P ; Sd <- T u + S-
+    double pm[NN];
+    sfor<0, NN>([&](auto J) {
+      constexpr int j = HD_K(J);
+      double t = 0.0;
+      sfor<0, NN>([&](auto K) { t = fma(am[HD_K(K)], bc<HD_K(K)>(tr[j]), t); });
+      pm[j] = t;
+    });
+    sfor<0, NN>([&](auto J) {
+      constexpr int j = HD_K(J);
+      double t = rl[j];
+      sfor<0, NN>([&](auto K) { t = fma(tr[HD_K(K)], bc<HD_K(K)>(pm[j]), t); });
+      ra[j] = t;
+    });
+    {
+      double t = sml;
+      sfor<0, NN>([&](auto K) { t = fma(tr[HD_K(K)], bc<HD_K(K)>(u), t); });
+      sd = t;
+    }
+    tauc += rec[2 * NN * NN + 2 * NN];
+  }
+
+  // ---- Lambertian surface: I+ = g x ----
+  double rgrow = 0.0;
+  sfor<0, NN>([&](auto J) { rgrow = fma(ra[HD_K(J)], Qc.g[HD_K(J)], rgrow); });
+  const double gsd = bc<0>(team_sum(g_i * sd));
+  const double grg = bc<0>(team_sum(g_i * rgrow));
+  double esurf = (1.0 - alb) * bsurf;
+  const double dirsurf = f0mu0 * exp(-tauc * rmu0);
+  if (beam) esurf += alb * dirsurf / kPi;
+  const double x = (2.0 * alb * gsd + esurf) / (1.0 - 2.0 * alb * grg);
+  double ip = g_i * x;
+  double* fo = A.flux + (size_t)s * (L + 1) * 2;
+  double chk = 0.0;
+  {
+    const double up = team_sum(g_i * ip);
+    const double dn = team_sum(g_i * fma(rgrow, x, sd));
+    if (i == 0) {
+      fo[0] = twopi * up;
+      fo[1] = twopi * dn + dirsurf;
+      chk += fo[0] + fo[1];
+    }
+  }
+  // ---- back-substitution bottom -> top ----
+  for (int lc = L - 1; lc >= 0; --lc) {
+    const double* bp = A.bsub + ((size_t)lc * nsc + sl) * ne2t<NN>();
+    double nip = act ? bp[NN * NN + ii] : 0.0;
+    sfor<0, NN>([&](auto J) {
+      const double z = act ? bp[ii * NN + HD_K(J)] : 0.0;
+      nip = fma(z, bc<HD_K(J)>(ip), nip);
+    });
+    const double rc = act ? bp[NN * NN + NN + ii] : 0.0;
+    const double up = team_sum(g_i * nip);
+    const double dn = team_sum(rc * nip);
+    ip = nip;
+    if (i == 0) {
+      const int lev = L - lc;
+      fo[2 * lev] = twopi * up;
+      fo[2 * lev + 1] = bp[NN * NN + 2 * NN] + dn;
+      chk += fo[2 * lev] + fo[2 * lev + 1];
+    }
+  }
+  if (!isfinite(chk)) st |= kStNonFinite;
+  if (st) {
+    atomicOr(&A.status[s], st);
+    if (st & 0x0F) atomicOr(A.anyerr, 1);
+  }
+}
+
+// ============================================================================
+// host side
+// ============================================================================
+template <int NN>
+static void fill_quad_team(Quad<NN>& q, const QuadHost& h) {
+  for (int i = 0; i < NN; ++i) {
+    q.mu[i] = h.mu[i];
+    q.w[i] = h.w[i];
+    q.sd[i] = h.sd[i];
+    q.g[i] = h.g[i];
+    q.rmu[i] = 1.0 / h.mu[i];
+    q.rg[i] = 1.0 / h.g[i];
+    for (int l = 0; l < 2 * NN; ++l) q.pt[l][i] = h.pt[l][i];
+  }
+}
+
+hipError_t upload_quad_tables_team(const QuadHost* per_nn /* [kMaxNN], index nn-1 */) {
+  QuadTablesTeam t;
+  fill_quad_team<9>(t.q9, per_nn[8]);
+  fill_quad_team<10>(t.q10, per_nn[9]);
+  fill_quad_team<11>(t.q11, per_nn[10]);
+  fill_quad_team<12>(t.q12, per_nn[11]);
+  fill_quad_team<13>(t.q13, per_nn[12]);
+  fill_quad_team<14>(t.q14, per_nn[13]);
+  fill_quad_team<15>(t.q15, per_nn[14]);
+  fill_quad_team<16>(t.q16, per_nn[15]);
+  return hipMemcpyToSymbol(HIP_SYMBOL(c_quad_team), &t, sizeof(t), 0, hipMemcpyHostToDevice);
+}
+
+template <int NN>
+static hipError_t launch_team(const PlanckArgs* pa, const TaucArgs* ta, const LayerArgs& la,
+                              const SweepArgs& sa, hipStream_t stream, hipEvent_t* ev) {
+  static_assert(ne1t<NN>() % 2 == 0 && ne2t<NN>() % 2 == 0, "16-byte aligned records");
+  launch_prologue(pa, ta, stream);
+  const long nt1 = (long)la.nsc * la.nlyr;
+  const unsigned nb1 = (unsigned)((nt1 + kTeamsPerBlock - 1) / kTeamsPerBlock);
+  const unsigned nb2 = (unsigned)((sa.nsc + kTeamsPerBlock - 1) / kTeamsPerBlock);
+  if (ev) (void)hipEventRecord(ev[0], stream);
+  hipLaunchKernelGGL(hd_team_layer_kernel<NN>, dim3(nb1), dim3(kTeamBlock), 0, stream, la);
+  if (ev) (void)hipEventRecord(ev[1], stream);
+  hipLaunchKernelGGL(hd_team_sweep_kernel<NN>, dim3(nb2), dim3(kTeamBlock), 0, stream, sa);
+  if (ev) (void)hipEventRecord(ev[2], stream);
+  return hipGetLastError();
+}
+
+hipError_t launch_solve_chunk_team(int nn, const PlanckArgs* pa, const TaucArgs* ta,
+                                   const LayerArgs& la, const SweepArgs& sa, hipStream_t stream,
+                                   hipEvent_t* ev) {
+  switch (nn) {
+    case 9: return launch_team<9>(pa, ta, la, sa, stream, ev);
+    case 10: return launch_team<10>(pa, ta, la, sa, stream, ev);
+    case 11: return launch_team<11>(pa, ta, la, sa, stream, ev);
+    case 12: return launch_team<12>(pa, ta, la, sa, stream, ev);
+    case 13: return launch_team<13>(pa, ta, la, sa, stream, ev);
+    case 14: return launch_team<14>(pa, ta, la, sa, stream, ev);
+    case 15: return launch_team<15>(pa, ta, la, sa, stream, ev);
+    case 16: return launch_team<16>(pa, ta, la, sa, stream, ev);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace hd

@@ -121,8 +121,8 @@ class Disort(RTSolver):
         if unknown:
             raise RuntimeError(f"Disort: unknown flags {sorted(unknown)}")
         ds = op.ds()
-        if ds.nstr < 2 or ds.nstr % 2 or ds.nstr > 16:
-            raise RuntimeError(f"Disort: nstr={ds.nstr} must be even and in [2, 16]")
+        if ds.nstr < 2 or ds.nstr % 2 or ds.nstr > 32:
+            raise RuntimeError(f"Disort: nstr={ds.nstr} must be even and in [2, 32]")
         if ds.nlyr < 1:
             raise RuntimeError(f"Disort: nlyr={ds.nlyr} must be >= 1")
         if "lamber" not in flags:

@@ -96,7 +96,7 @@ def _random_batch(rng, nwave, ncol, nlyr, nstr, planck, beam=True, ssa_max=0.99,
     return prop, bc, kw
 
 
-@pytest.mark.parametrize("nstr", [2, 4, 6, 8, 10, 12, 14, 16])
+@pytest.mark.parametrize("nstr", [2, 4, 6, 8, 10, 12, 14, 16, 18, 20, 22, 24, 26, 28, 30, 32])
 @pytest.mark.parametrize("planck", [False, True])
 def test_vs_c_oracle(oracle_c, nstr, planck):
     rng = np.random.default_rng(1000 + nstr + 100 * planck)
@@ -128,6 +128,46 @@ def test_headline_config_subsample(oracle_c):
     assert err < TOL, f"max rel err {err:.3e}"
 
 
+def test_aerosol_config_subsample(oracle_c):
+    """C5 shape (nstr=32, nmom=32, nlyr=80, omega in [0.9, 0.9999],
+    HG g in [0.6, 0.9] so delta-M is active, umu0 in [0.1, 1]): the 16-lane
+    team kernels vs the C oracle on a 64-solve subsample of a 512-solve slab."""
+    rng = np.random.default_rng(20250218)
+    nwave, ncol, nlyr, nstr = 4, 128, 80, 32
+    prop = np.zeros((nwave, ncol, nlyr, 2 + nstr))
+    prop[..., 0] = 10.0 ** rng.uniform(-5, 0.7, (nwave, ncol, nlyr))
+    prop[..., 1] = rng.uniform(0.9, 0.9999, (nwave, ncol, nlyr))
+    g = rng.uniform(0.6, 0.9, (nwave, ncol, nlyr))
+    for l in range(nstr):
+        prop[..., 2 + l] = g ** (l + 1)
+    bc = {"fbeam": np.ones((nwave, ncol)), "umu0": rng.uniform(0.1, 1.0, (nwave, ncol)),
+          "albedo": rng.uniform(0, 1, (nwave, ncol))}
+    d = _disort(nstr, nlyr, nwave, ncol)
+    f = _run(d, prop, bc)
+    idx = rng.choice(nwave * ncol, 64, replace=False)
+    ref = np.zeros_like(f)
+    for s in idx:
+        oracle_c.forward(prop, bc, nstr=nstr, first=int(s), count=1, out=ref)
+    err = rel_err(f.reshape(-1, nlyr + 1, 2)[idx], ref.reshape(-1, nlyr + 1, 2)[idx]).max()
+    assert err < TOL, f"max rel err {err:.3e}"
+
+
+@pytest.mark.parametrize("nstr", [8, 24])
+def test_chunking_invariance_team(nstr):
+    rng = np.random.default_rng(70 + nstr)
+    prop, bc, _ = _random_batch(rng, 3, 37, 12, nstr, False)
+    d = _disort(nstr, 12, 3, 37)
+    f1 = _run(d, prop, bc)
+    from pyharp_amd.disort import _context
+    ctx = _context(0)
+    ctx.set_chunk(17)
+    try:
+        f2 = _run(d, prop, bc)
+    finally:
+        ctx.set_chunk(0)
+    assert np.array_equal(f1, f2)
+
+
 def test_chunking_invariance():
     rng = np.random.default_rng(7)
     prop, bc, _ = _random_batch(rng, 3, 37, 20, 8, False)
@@ -153,11 +193,12 @@ def test_linearity_in_fbeam():
     assert rel_err(f3, 3.0 * f1).max() < 1e-12
 
 
-def test_conservative_energy_balance():
+@pytest.mark.parametrize("nstr", [16, 32])
+def test_conservative_energy_balance(nstr):
     """omega=1 everywhere, albedo=1, beam only: net flux ~0 at every level
     (exact but for DISORT's dither of ssalb=1 -> 1-4.7e-8)."""
     rng = np.random.default_rng(9)
-    nwave, ncol, nlyr, nstr = 2, 8, 25, 16
+    nwave, ncol, nlyr = 2, 8, 25
     prop, bc, _ = _random_batch(rng, nwave, ncol, nlyr, nstr, False)
     prop[..., 1] = 1.0
     bc["albedo"] = np.ones((nwave, ncol))
