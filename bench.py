@@ -1,21 +1,26 @@
 """Benchmark of the DISORT flux hot path on MI355X (driver contract).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--planck] [--ncol C]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c5] [--planck]
+                    [--ncol C] [--ngpoint G]
 
-Workload (BASELINE.json configs[3], SURVEY.md 8(d) "C4 GCM"): 1e4 synthetic
-columns x 64 g-points, nstr=16, nmom=16 (Henyey-Greenstein chi_l = g^l),
-nlyr=80, tau log-uniform [1e-5, 5], omega in [0, 0.99], g in [0, 0.85],
-umu0 in [0.05, 1], albedo in [0, 1], fbeam = 1 (``--planck`` adds thermal
-emission, T 150-300 K).  One step = one flux solve of every (g-point, column)
-pair of the rank's shard (hd_solve through the C-ABI) + the g-weighted band
-flux (C, L+1, 2), all-reduced over ranks.  Inputs are generated on the device
-before the timed region (seeded per g-point, so the global problem does not
-depend on N).  Spectral sharding: rank r owns g-points {g : g mod N == r}
-(fixed global problem -> "scaling": "strong").
+Default workload (BASELINE.json configs[3], SURVEY.md 8(d) "C4 GCM", the
+configuration the metric is quoted on): 1e4 synthetic columns x 64 g-points,
+nstr=16, nmom=16 (Henyey-Greenstein chi_l = g^l), nlyr=80, tau log-uniform
+[1e-5, 5], omega in [0, 0.99], g in [0, 0.85], umu0 in [0.05, 1], albedo in
+[0, 1], fbeam = 1 (``--planck`` adds thermal emission, T 150-300 K).
+``--config c5`` is SURVEY 8(d) "C5 aerosol" (BASELINE.json configs[4]):
+1e3 columns x 64 g-points, nstr=32, nmom=32, nlyr=80, omega in [0.9, 0.9999],
+g in [0.6, 0.9] (delta-M active), umu0 in [0.1, 1].
+One step = one flux solve of every (g-point, column) pair of the rank's shard
+(hd_solve through the C-ABI) + the g-weighted band flux (C, L+1, 2),
+all-reduced over ranks.  Inputs are generated on the device before the timed
+region (seeded per g-point, so the global problem does not depend on N).
+Spectral sharding: rank r owns g-points {g : g mod N == r} (fixed global
+problem -> "scaling": "strong").
 
 Printed (rank 0): one JSON line with the contract fields plus
-  roofline      dominant kernel (hd_layer_kernel), algorithmic FLOP per launch
-                / average launch time from HIP events on the solve stream
+  roofline      dominant kernel (the layer-setup kernel), algorithmic FLOP per
+                launch / average launch time from HIP events on the solve stream
   cpu_baseline  oracle/ C restatement (a port of the DISORT algorithm, not
                 cdisort, which is absent) timed on the host cores, N=1 only
   max_rel_err   GPU vs that CPU restatement on a subsample of the workload
@@ -57,8 +62,18 @@ def algorithmic_flop(nstr: int, nlyr: int, planck: bool):
     return total, k1, k2
 
 
-def make_inputs(gpoints, ncol, nlyr, nstr, planck, dev, seed=20250217):
-    """Synthetic C4 inputs for the given g-points, generated on `dev`."""
+CONFIGS = {
+    # name: ncol, ngpoint, nstr, nlyr, (ssa lo, hi), (g lo, hi), (umu0 lo, hi), label
+    "c4": dict(ncol=10000, ngpoint=64, nstr=16, nlyr=80, ssa=(0.0, 0.99), g=(0.0, 0.85),
+               umu0=(0.05, 1.0), label="C4 GCM batch"),
+    "c5": dict(ncol=1000, ngpoint=64, nstr=32, nlyr=80, ssa=(0.9, 0.9999), g=(0.6, 0.9),
+               umu0=(0.1, 1.0), label="C5 high-scatter aerosol"),
+}
+
+
+def make_inputs(gpoints, ncol, nlyr, nstr, planck, dev, seed=20250217, ssa=(0.0, 0.99),
+                gasym=(0.0, 0.85), umu0=(0.05, 1.0)):
+    """Synthetic inputs (SURVEY 8(d) distributions) for the given g-points, on `dev`."""
     nmom = nstr
     W = len(gpoints)
     f64 = torch.float64
@@ -71,12 +86,12 @@ def make_inputs(gpoints, ncol, nlyr, nstr, planck, dev, seed=20250217):
         gen.manual_seed(seed * 1000 + int(g))
         r = lambda *shape: torch.rand(shape, generator=gen, dtype=f64, device=dev)  # noqa: E731
         prop[i, ..., 0] = 10.0 ** (r(ncol, nlyr) * np.log10(5.0 / 1e-5) - 5.0)
-        prop[i, ..., 1] = 0.99 * r(ncol, nlyr)
-        gg = 0.85 * r(ncol, nlyr)
+        prop[i, ..., 1] = ssa[0] + (ssa[1] - ssa[0]) * r(ncol, nlyr)
+        gg = gasym[0] + (gasym[1] - gasym[0]) * r(ncol, nlyr)
         for l in range(nmom):
             prop[i, ..., 2 + l] = gg ** (l + 1)
         bc["fbeam"][i] = 1.0
-        bc["umu0"][i] = 0.05 + 0.95 * r(ncol)
+        bc["umu0"][i] = umu0[0] + (umu0[1] - umu0[0]) * r(ncol)
         bc["albedo"][i] = r(ncol)
         if planck:
             bc["btemp"][i] = 300.0
@@ -150,13 +165,18 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--ncol", type=int, default=10000)
-    ap.add_argument("--ngpoint", type=int, default=64)
-    ap.add_argument("--nlyr", type=int, default=80)
-    ap.add_argument("--nstr", type=int, default=16)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c4")
+    ap.add_argument("--ncol", type=int, default=None)
+    ap.add_argument("--ngpoint", type=int, default=None)
+    ap.add_argument("--nlyr", type=int, default=None)
+    ap.add_argument("--nstr", type=int, default=None)
     ap.add_argument("--planck", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    cfgd = CONFIGS[args.config]
+    for k in ("ncol", "ngpoint", "nlyr", "nstr"):
+        if getattr(args, k) is None:
+            setattr(args, k, cfgd[k])
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -178,7 +198,8 @@ def main():
     W = len(gpoints)
     wl_all, wu_all = wave_bounds(G)
     wl, wu = wl_all[gpoints], wu_all[gpoints]
-    prop, bc, temf = make_inputs(gpoints, ncol, nlyr, nstr, args.planck, dev)
+    prop, bc, temf = make_inputs(gpoints, ncol, nlyr, nstr, args.planck, dev,
+                                 ssa=cfgd["ssa"], gasym=cfgd["g"], umu0=cfgd["umu0"])
     wts = torch.tensor(gpoint_weights(G)[gpoints], dtype=torch.float64, device=dev)
 
     op = DisortOptions().flags("lamber,quiet,onlyfl" + (",planck" if args.planck else ""))
@@ -222,21 +243,22 @@ def main():
     nsolve_total = G * ncol
     value = nsolve_total * args.steps / elapsed
     total_flop, k1_flop, k2_flop = algorithmic_flop(nstr, nlyr, args.planck)
-    workload = (f"C4 GCM batch: {ncol} columns x {G} g-points, nstr={nstr}, nmom={nstr}, "
+    workload = (f"{cfgd['label']}: {ncol} columns x {G} g-points, nstr={nstr}, nmom={nstr}, "
                 f"nlyr={nlyr}, beam{' + planck' if args.planck else ''}")
 
+    layer_kernel = "hd_layer_kernel" if nstr <= 16 else "hd_team_layer_kernel"
     if rank == 0:
-        # dominant kernel roofline (hd_layer_kernel), per launch
+        # dominant kernel roofline (the layer-setup kernel), per launch
         k1_avg_ms = tm.layer_ms / max(tm.layer_launches, 1)
         solves_per_launch = W * ncol * args.steps / max(tm.layer_launches, 1)
         ach = k1_flop * solves_per_launch / (k1_avg_ms * 1e-3) / 1e12
         pmc = load_pmc(nstr, nlyr, args.planck)
         traffic = None
         if pmc:
-            k1 = pmc["kernels"].get(f"hd_layer_kernel<{nstr // 2}>")
+            k1 = pmc["kernels"].get(f"{layer_kernel}<{nstr // 2}>")
             if k1:
                 traffic = round(k1["bytes_per_solve"] * solves_per_launch)
-        roofline = {"bound": "mfma", "kernel": "hd_layer_kernel", "achieved": round(ach, 3),
+        roofline = {"bound": "mfma", "kernel": f"{layer_kernel}<{nstr // 2}>", "achieved": round(ach, 3),
                     "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(ach / FP64_PEAK_TFLOPS, 4),
                     "traffic": traffic,

@@ -205,86 +205,70 @@ __host__ __device__ constexpr bool round_has_pair(int m) {
   return false;
 }
 
+// One-sided (Hestenes) Jacobi on the columns of B: lane j holds column j of B
+// (b) and of V (vc).  Round M rotates the column pair (j, j^M) to make the two
+// orthogonal -- exactly the two-sided Jacobi rotation of B^T B for that pair,
+// built from column dot products -- so B^T B is never formed and no diagonal
+// has to be fished out of a lane-indexed register.  Both lanes of a pair form
+// their operands in the same order (products commute exactly), so the two
+// rotations agree bitwise.
+constexpr double kJacobiTol2 = 1.0e-30;  // (|b_p . b_q| / |b_p||b_q|)^2 threshold
+
 template <int NN, int M>
-__device__ __forceinline__ void team_jacobi_round(double (&a)[NN], double (&v)[NN], bool on) {
+__device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double (&vc)[NN], bool on,
+                                                  bool& rot_any) {
   const int i = tlane();
-  double cc[NN], ss[NN];
-  double c_own = 1.0, s_own = 0.0;  // this lane's pair; s carries the side's sign
-  sfor<0, NN>([&](auto P) {
-    constexpr int p = HD_K(P), q = p ^ M;
-    if constexpr (q > p && q < NN) {
-      // w = sqrt(d^2 + 4 a^2), u = |d| + w, z = 1/sqrt(2 w u): c = u z, s = sgn(d) 2 a z
-      const double app = bc<p>(a[p]), aqq = bc<q>(a[q]), apq = bc<p>(a[q]);
-      const double d = aqq - app;
-      const double w2 = fma(d, d, 4.0 * apq * apq);
-      const bool rot = on && w2 > 1.0e-280;
-      const double w2s = rot ? w2 : 1.0;
-      const double w = w2s * rsq_nr(w2s);
-      const double u = fabs(d) + w;
-      const double z = rsq_nr(2.0 * w * u);
-      const double sg = d < 0.0 ? -2.0 : 2.0;
-      const double c = rot ? u * z : 1.0;
-      const double s = rot ? sg * apq * z : 0.0;
-      cc[p] = c;
-      ss[p] = s;
-      if (i == p || i == q) c_own = c;
-      if (i == p) s_own = -s;
-      if (i == q) s_own = s;
-    }
+  const int pi = i ^ M;
+  double bq[NN], vq[NN];
+  sfor<0, NN>([&](auto K) {
+    constexpr int k = HD_K(K);
+    bq[k] = xperm<M>(b[k]);
+    vq[k] = xperm<M>(vc[k]);
   });
-  // B = A J, V <- V J (column rotations: lane-local)
-  sfor<0, NN>([&](auto P) {
-    constexpr int p = HD_K(P), q = p ^ M;
-    if constexpr (q > p && q < NN) {
-      const double c = cc[p], s = ss[p];
-      const double ap = a[p], aq = a[q];
-      a[p] = fma(c, ap, -s * aq);
-      a[q] = fma(s, ap, c * aq);
-      const double vp = v[p], vq = v[q];
-      v[p] = fma(c, vp, -s * vq);
-      v[q] = fma(s, vp, c * vq);
-    }
+  double own = 0.0, oth = 0.0, gam = 0.0;
+  sfor<0, NN>([&](auto K) {
+    constexpr int k = HD_K(K);
+    own = fma(b[k], b[k], own);
+    oth = fma(bq[k], bq[k], oth);
+    gam = fma(b[k], bq[k], gam);
   });
-  // A' = J^T B: row p' = c b_p - s b_q, row q' = s b_p + c b_q (partner = lane i^M)
-  sfor<0, NN>([&](auto J) {
-    constexpr int j = HD_K(J);
-    const double b = xperm<M>(a[j]);
-    a[j] = fma(s_own, b, c_own * a[j]);
+  const bool lo = i < pi;
+  const double app = lo ? own : oth;
+  const double aqq = lo ? oth : own;
+  const bool r = on && i < NN && pi < NN && gam * gam > kJacobiTol2 * app * aqq;
+  // w = sqrt(d^2 + 4 g^2), u = |d| + w, z = 1/sqrt(2 w u): c = u z, s = sgn(d) 2 g z
+  const double d = aqq - app;
+  const double w2 = r ? fma(d, d, 4.0 * gam * gam) : 1.0;
+  const double w = w2 * rsq_nr(w2);
+  const double u = fabs(d) + w;
+  const double z = rsq_nr(2.0 * w * u);
+  const double sg = d < 0.0 ? -2.0 : 2.0;
+  const double c = r ? u * z : 1.0;
+  const double s = r ? sg * gam * z : 0.0;
+  const double se = lo ? -s : s;  // p side: c b_p - s b_q ; q side: s b_p + c b_q
+  sfor<0, NN>([&](auto K) {
+    constexpr int k = HD_K(K);
+    b[k] = fma(se, bq[k], c * b[k]);
+    vc[k] = fma(se, vq[k], c * vc[k]);
   });
-  if (on) {  // the rotated pairs are zero by construction
-    sfor<0, NN>([&](auto P) {
-      constexpr int p = HD_K(P), q = p ^ M;
-      if constexpr (q > p && q < NN) {
-        if (i == p) a[q] = 0.0;
-        if (i == q) a[p] = 0.0;
-      }
-    });
-  }
+  rot_any = rot_any || r;
 }
 
-// a (rows of a symmetric matrix) -> eigenvalues on the diagonal, eigenvectors
-// in the columns of v (rows distributed).  A converged team stops rotating;
-// the loop ends when every team of the wave has converged or after max_sweeps.
+// Sweeps of rounds 1..15 until a sweep rotates nothing in any team of the wave
+// (a converged team keeps issuing no-op rotations) or max_sweeps.
 template <int NN>
-__device__ __forceinline__ void team_jacobi(double (&a)[NN], double (&v)[NN], int max_sweeps) {
+__device__ __forceinline__ void team_jacobi(double (&b)[NN], double (&vc)[NN], int max_sweeps) {
   const int i = tlane();
-  sfor<0, NN>([&](auto J) { v[HD_K(J)] = i == HD_K(J) ? 1.0 : 0.0; });
+  sfor<0, NN>([&](auto J) { vc[HD_K(J)] = i == HD_K(J) ? 1.0 : 0.0; });
+  bool on = true;
   for (int sweep = 0; sweep < max_sweeps; ++sweep) {
-    double off = 0.0, dia = 0.0;
-    sfor<0, NN>([&](auto J) {
-      constexpr int j = HD_K(J);
-      const double x2 = a[j] * a[j];
-      if (i == j) dia += x2;
-      else off += x2;
-    });
-    off = bc<0>(team_sum(off));
-    dia = bc<0>(team_sum(dia));
-    const bool done = !(off > 2.0e-30 * dia);  // both triangles: the 1e-30 of jacobi_eig
-    if (__all(done)) break;
+    bool rot_any = false;
     sfor<1, kTeam>([&](auto Mc) {
       constexpr int m = HD_K(Mc);
-      if constexpr (round_has_pair<NN>(m)) team_jacobi_round<NN, m>(a, v, !done);
+      if constexpr (round_has_pair<NN>(m)) team_jacobi_round<NN, m>(b, vc, on, rot_any);
     });
+    on = bc<0>(team_sum(rot_any ? 1.0 : 0.0)) > 0.0;
+    if (__all(!on)) break;
   }
 }
 
@@ -414,41 +398,35 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_layer_kernel(LayerArgs A) 
     cvec = act ? fma(b1 * rg_i, cvec, db) : 0.0;
   }
 
-  // ---- Sym = L^T (-A+) L ----
-  double sym[NN];
+  // ---- eigenpairs (c_soleig): Sym = L^T (-A+) L = V diag(k^2) V^T ----
+  // With C C^T = -A+ (SPD because Sym is), Sym = B^T B for B = C^T L; the
+  // one-sided Jacobi on B's columns yields k^2 = |b_j|^2 and V.
+  double vt[NN];  // lane j: column j of V (row j of V^T)
+  double kk;      // lane j: k_j
   {
-    double m[NN];
-    sfor<0, NN>([&](auto J) {
-      constexpr int j = HD_K(J);
+    double unused[NN], rdc;
+    if (!team_chol<NN, false>(ap, unused, rdc)) st |= kStEigen;  // ap <- rows of C
+    double bcol[NN];  // lane j: B_ij = sum_k C_ki L_kj
+    sfor<0, NN>([&](auto I) {
+      constexpr int r = HD_K(I);
       double t = 0.0;
-      sfor<j, NN>([&](auto K) { t = fma(ap[HD_K(K)], bc<HD_K(K)>(lch[j]), t); });
-      m[j] = t;
+      sfor<r, NN>([&](auto K) { t = fma(bc<HD_K(K)>(ap[r]), lt[HD_K(K)], t); });
+      bcol[r] = t;
     });
-    sfor<0, NN>([&](auto J) {
-      constexpr int j = HD_K(J);
-      double t = 0.0;
-      sfor<0, NN>([&](auto K) { t = fma(lt[HD_K(K)], bc<HD_K(K)>(m[j]), t); });
-      sym[j] = t;
-    });
+    team_jacobi<NN>(bcol, vt, A.max_sweeps);
+    double k2 = 0.0;
+    sfor<0, NN>([&](auto K) { k2 = fma(bcol[HD_K(K)], bcol[HD_K(K)], k2); });
+    if (act && !(k2 > 0.0)) st |= kStEigen;
+    kk = act ? sqrt(k2 > 0.0 ? k2 : 0.0) : 0.0;
   }
-
-  // ---- eigenpairs (c_soleig): Sym = V diag(k^2) V^T ----
+  // v = rows of V (lane i: V_ij over j)
   double v[NN];
-  team_jacobi<NN>(sym, v, A.max_sweeps);
-  double k2 = 0.0;
   sfor<0, NN>([&](auto J) {
-    if (i == HD_K(J)) k2 = sym[HD_K(J)];
-  });
-  if (act && !(k2 > 0.0)) st |= kStEigen;
-  const double kk = sqrt(k2 > 0.0 ? k2 : 0.0);  // lane j: eigenvalue of column j
-  // vt = V^T rows (lane j: column j of V)
-  double vt[NN];
-  sfor<0, NN>([&](auto Ai) {
-    constexpr int a = HD_K(Ai);
-    vt[a] = 0.0;
-    sfor<0, NN>([&](auto J) {
-      const double x = bc<a>(v[HD_K(J)]);
-      if (i == HD_K(J)) vt[a] = x;
+    constexpr int j = HD_K(J);
+    v[j] = 0.0;
+    sfor<0, NN>([&](auto I) {
+      const double x = bc<j>(vt[HD_K(I)]);
+      if (i == HD_K(I)) v[j] = x;
     });
   });
 
