@@ -1,0 +1,82 @@
+/*
+ * hdharp.h -- C-ABI of the harp-side steps on either side of the DISORT flux
+ * solve (part of libhdisort.so; HIP kernels for gfx950, include/hdisort.h
+ * for the solve itself).  SURVEY.md section 8(f) ranks 1 and 2:
+ *
+ *   before the solve -- optics assembly straight into the solver layout:
+ *     hd_attenuate     one attenuator's forward: S8FullerImpl::forward
+ *                      (src/opacity/s8_fuller.cpp:72-117) and
+ *                      H2SO4SimpleImpl::forward (src/opacity/h2so4_simple.cpp:72-117):
+ *                      1-D linear interpolation of (k_ext, ssa) in wavelength
+ *                      (src/math/interpn.h:34-76, locate.h:15-42, clamped at the
+ *                      table ends), times the species concentration
+ *     hd_band_optics   the amars_sw assembly (examples/amars_sw.cpp:261-271):
+ *                      sum of attenuators, x dz, ssa = sum(ssa k c)/sum(k c),
+ *                      written as prop [nwave][ncol][nlyr][nprop]
+ *   after the solve -- band epilogue:
+ *     hd_band_flux     sum_w weight_w F_w (examples/amars_lw.cpp:84-88;
+ *                      amars_sw.cpp:169-196 with weight = d(wavenumber);
+ *                      legacy src/rtsolver/rt_solver_disort.cpp_:183-184)
+ *     hd_heating_rate  dT/dt = -(dF_net/dz)/(rho c_p), F_net = F_up - F_dn
+ *                      (examples/amars_sw.cpp:291-302)
+ *     hd_spherical_flux_correction  src/utils/spherical_flux_correction.cpp:3-17
+ *                      along the level axis of the harp band flux
+ *                      (legacy rt_solver_disort.cpp_:186-207)
+ *
+ * All array pointers are DEVICE pointers; stream = hipStream_t (NULL =
+ * default).  Return codes and hd_last_error(NULL) as in hdisort.h.
+ */
+#ifndef HDHARP_H_
+#define HDHARP_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* one opacity table, already in the units the reference keeps after reset():
+ * k_ext multiplied by the species weight [m^2/kg -> m^2/mol]
+ * (s8_fuller.cpp:64-66, h2so4_simple.cpp:64-66) */
+typedef struct hd_attenuator {
+  int nrow;                 /* table rows, wavelength strictly monotonic         */
+  const double *wavelength; /* [nrow] um (first data column of the text table)   */
+  const double *kext;       /* [nrow] extinction cross-section, m^2/mol          */
+  const double *ssa;        /* [nrow] single-scattering albedo                   */
+  int species;              /* index into the last dim of conc                   */
+} hd_attenuator;
+
+/* coordinate kinds: kwargs["wavelength"] [um] or kwargs["wavenumber"] [cm^-1]
+ * (wavelength = 1e4 / wavenumber, s8_fuller.cpp:79-85) */
+#define HD_COORD_WAVELENGTH 0
+#define HD_COORD_WAVENUMBER 1
+
+/* out [nwave][ncol][nlyr][2]: [0] = k(lambda) c, [1] = ssa(lambda) k(lambda) c
+ * conc [ncol][nlyr][nspecies] mol/m^3 */
+int hd_attenuate(const hd_attenuator *att, const double *coord, int coord_kind, int nwave,
+                 const double *conc, int ncol, int nlyr, int nspecies, double *out,
+                 void *stream);
+
+/* prop [nwave][ncol][nlyr][nprop] (nprop >= 2): [0] = dz sum_a k_a c_a (layer
+ * optical thickness), [1] = sum_a ssa_a k_a c_a / sum_a k_a c_a (0 where the
+ * layer has no extinction; the reference divides 0/0 there), [2..] = 0.
+ * dz [ncol][nlyr] m */
+int hd_band_optics(const hd_attenuator *atts, int natt, const double *coord, int coord_kind,
+                   int nwave, const double *conc, int ncol, int nlyr, int nspecies,
+                   const double *dz, int nprop, double *prop, void *stream);
+
+/* bflux [ncol][nlev][2] = sum_w weight[w] flux[w][ncol][nlev][2] (fixed order) */
+int hd_band_flux(const double *flux, const double *weight, int nwave, int ncol, int nlev,
+                 double *bflux, void *stream);
+
+/* dTdt [ncol][nlyr] K/s from bflux [ncol][nlyr+1][2], dz and rho [ncol][nlyr] */
+int hd_heating_rate(const double *bflux, const double *dz, const double *rho, double cp,
+                    int ncol, int nlyr, double *dTdt, void *stream);
+
+/* in place on bflux [ncol][nlev][2] (both directions); x1f, area [nlev],
+ * vol [nlev-1], level 0 = bottom as in harp */
+int hd_spherical_flux_correction(double *bflux, const double *x1f, const double *area,
+                                 const double *vol, int ncol, int nlev, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HDHARP_H_ */

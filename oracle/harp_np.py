@@ -1,0 +1,206 @@
+"""CPU restatement (numpy, TEST INFRASTRUCTURE ONLY) of the harp-side steps on
+either side of the DISORT solve, for the parity tests of include/hdharp.h.
+
+Nothing in pyharp_amd/ imports this module; it is the checker, never the
+thing measured or shipped.  Each function cites the reference code it follows
+(/root/reference at the survey snapshot).
+
+Parity status: the reference's tests for these steps (tests/test_attenuator.cpp)
+print without asserting, and the reference sources need the CMake-generated
+configure.h, so they are not built here.  The restatement is pinned by
+closed-form properties in tests/test_harp_oracle.py (exact table values at the
+nodes, linearity between them, clamping outside, constant-spacing band sums)
+and by the amars_sw example's own quantitative statement that the integrated
+TOA downward flux is within 2 W/m^2 of 410 W/m^2 (examples/amars_sw.cpp:75-77).
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+
+def locate(xx, x):
+    """src/math/locate.h:15-42 (Numerical Recipes locate), zero-offset result:
+    j with xx[j] <= x < xx[j+1]; -1 below, n-1 at/above the last node."""
+    n = len(xx)
+    jl, ju = 0, n + 1
+    ascnd = xx[n - 1] >= xx[0]
+    while ju - jl > 1:
+        jm = (ju + jl) >> 1
+        if (x >= xx[jm - 1]) == ascnd:
+            jl = jm
+        else:
+            ju = jm
+    if x == xx[0]:
+        j = 1
+    elif x == xx[n - 1]:
+        j = n
+    else:
+        j = jl
+    return j - 1
+
+
+def interp1(x, axis, data):
+    """src/math/interpn.h:34-76 with ndim = 1: data (rows, nval) -> (nval,)."""
+    n = len(axis)
+    i1 = locate(axis, x)
+    if i1 == -1:
+        i1 = i2 = 0
+    elif i1 == n - 1:
+        i2 = n - 1
+    else:
+        i2 = i1 + 1
+    x1, x2 = axis[i1], axis[i2]
+    v1, v2 = data[i1], data[i2]
+    if x2 != x1:
+        return ((x - x1) * v2 + (x2 - x) * v1) / (x2 - x1)
+    return (v1 + v2) / 2.0
+
+
+def read_table(path):
+    """src/utils/fileio.cpp decomment_file + the 2-pass read of s8_fuller.cpp:29-62."""
+    rows = []
+    with open(path) as f:
+        for line in f:
+            line = line.split("#", 1)[0].strip()
+            if line:
+                rows.append([float(v) for v in line.split()])
+    return np.asarray(rows, dtype=np.float64)
+
+
+def load_attenuator(path, species_weight):
+    """(kwave [um], kdata (rows, 2)) after reset(): k_ext *= species weight
+    (s8_fuller.cpp:64-66)."""
+    t = read_table(path)
+    kdata = t[:, 1:].copy()
+    kdata[:, 0] *= species_weight
+    return t[:, 0].copy(), kdata
+
+
+def attenuate(kwave, kdata, species, conc, wavenumber=None, wavelength=None):
+    """S8FullerImpl::forward (s8_fuller.cpp:72-117): (nwave, ncol, nlyr, 2)."""
+    coord = 1.0e4 / np.asarray(wavenumber) if wavelength is None else np.asarray(wavelength)
+    ncol, nlyr, _ = conc.shape
+    out = np.zeros((len(coord), ncol, nlyr, 2))
+    c = conc[:, :, species]
+    for w, x in enumerate(coord):
+        k, s = interp1(x, kwave, kdata)
+        kc = k * c
+        out[w, :, :, 0] = kc
+        out[w, :, :, 1] = s * kc
+    return out
+
+
+def band_optics(tables, conc, dz, nprop=2, wavenumber=None, wavelength=None):
+    """examples/amars_sw.cpp:261-271: prop = sum_a attenuate_a; prop *= dz;
+    prop[...,1] /= prop[...,0] (0 where tau = 0).  tables: [(kwave, kdata, species)]."""
+    ncol, nlyr, _ = conc.shape
+    dz = np.broadcast_to(np.asarray(dz, np.float64).reshape(-1, nlyr), (ncol, nlyr))
+    tot = None
+    for kwave, kdata, sp in tables:
+        a = attenuate(kwave, kdata, sp, conc, wavenumber, wavelength)
+        tot = a if tot is None else tot + a
+    tot = tot * dz[None, :, :, None]
+    prop = np.zeros(tot.shape[:3] + (nprop,))
+    prop[..., 0] = tot[..., 0]
+    with np.errstate(invalid="ignore", divide="ignore"):
+        prop[..., 1] = np.where(tot[..., 0] != 0.0, tot[..., 1] / tot[..., 0], 0.0)
+    return prop
+
+
+def band_flux(flux, weight):
+    """sum_w weight_w F_w in w order (amars_lw.cpp:84-88)."""
+    out = np.zeros(flux.shape[1:])
+    for w in range(flux.shape[0]):
+        out = weight[w] * flux[w] + out
+    return out
+
+
+def heating_rate(bflux, dz, rho, cp):
+    """examples/amars_sw.cpp:291-302: dT/dt[k] = -(1/(rho_k cp)) (dF[k+1]-dF[k])/dz_k,
+    dF = F_up - F_dn, level 0 = bottom.  bflux (ncol, nlyr+1, 2)."""
+    df = bflux[..., 0] - bflux[..., 1]
+    ncol, nlev = df.shape
+    dz = np.broadcast_to(dz, (ncol, nlev - 1))
+    rho = np.broadcast_to(rho, (ncol, nlev - 1))
+    return -(1.0 / (rho * cp)) * (df[:, 1:] - df[:, :-1]) / dz
+
+
+def spherical_flux_correction(bflux, x1f, area, vol):
+    """src/utils/spherical_flux_correction.cpp:3-17 along the level axis of the
+    harp band flux (ncol, nlev, 2); returns a corrected copy."""
+    f = np.array(bflux, dtype=np.float64, copy=True)
+    nlev = f.shape[1]
+    fiu = f[:, nlev - 1, :].copy()
+    for i in range(nlev - 2, -1, -1):
+        dx1f = x1f[i + 1] - x1f[i]
+        fi = f[:, i, :].copy()
+        volh = (fiu - fi) / dx1f * vol[i]
+        fiu = fi
+        f[:, i, :] = (f[:, i + 1, :] * area[i + 1] - volh) / area[i]
+    return f
+
+
+# ---- the amars_sw example's own helpers (examples/amars_sw.cpp) -------------
+
+def short_wavenumber_grid(nwave):
+    """amars_sw.cpp:70-76."""
+    return np.linspace(2000.0, 50000.0, nwave)
+
+
+def bb_toa_flux(wave, ncol, temp, fscale):
+    """amars_sw.cpp:84-102: scaled blackbody TOA flux [W/(m^2 cm^-1)]."""
+    c1 = 1.19144e-5 * 1e-3
+    c2 = 1.4388
+    sr_sun = 2.92842e-5
+    f = fscale * sr_sun * c1 * wave ** 3 / (np.exp(c2 * wave / temp) - 1.0)
+    return np.repeat(f[:, None], ncol, axis=1)
+
+
+def read_aerosol_profile(path):
+    """amars_sw.cpp:104-126 + 228-239: p [Pa], T [K], mixing ratios (2, n)."""
+    t = read_table(path)
+    return t[:, 0] * 1e5, t[:, 1].copy(), np.stack([t[:, 2], t[:, 3]])
+
+
+def regrid_ptx(nlyr, p, T, mr):
+    """amars_sw.cpp:128-152: uniform p and T grids (top first), mixing ratios
+    interpolated in p with interp1 (interpolate_mixing_ratios, :24-36)."""
+    p_min, p_max = p.min(), p.max()
+    T_min, T_max = T.min(), T.max()
+    p_step = (p_max - p_min) / (nlyr - 1)
+    T_step = (T_max - T_min) / (nlyr - 1)
+    new_p = np.zeros(nlyr)
+    new_T = np.zeros(nlyr)
+    for i in range(nlyr):
+        new_p[nlyr - 1 - i] = p_min + i * p_step
+        new_T[nlyr - 1 - i] = T_min + i * T_step
+    new_mr = np.zeros((mr.shape[0], nlyr))
+    for j in range(mr.shape[0]):
+        for i in range(nlyr):
+            new_mr[j, i] = interp1(new_p[i], p, mr[j][:, None])[0]
+    return new_p, new_T, new_mr
+
+
+def calc_dz(nlyr, new_p, new_rho, g):
+    """amars_sw.cpp:154-170 (the last layer is twice the one below it)."""
+    dz = np.ones(nlyr)
+    for i in range(nlyr - 1):
+        dz[i] *= (new_p[i] - new_p[i + 1]) / (g * new_rho[i])
+    dz[nlyr - 1] *= 2 * dz[nlyr - 2]
+    return dz
+
+
+def amars_sw_atmosphere(profile_path, nlyr=40, g=3.711, mean_mol_weight=0.044, R=8.314472):
+    """conc (1, nlyr, 2) [mol/m^3] (S8 = species 0, H2SO4 = 1), rho, dz, p
+    (amars_sw.cpp:228-258)."""
+    p, T, mr = read_aerosol_profile(profile_path)
+    new_p, new_T, new_mr = regrid_ptx(nlyr, p, T, mr)
+    conc = np.ones((1, nlyr, 2))
+    new_rho = np.zeros(nlyr)
+    for k in range(nlyr):
+        conc[0, k, 0] = (new_mr[1, k] * new_p[k]) / (R * new_T[k])
+        conc[0, k, 1] = (new_mr[0, k] * new_p[k]) / (R * new_T[k])
+        new_rho[k] = (new_p[k] * mean_mol_weight) / (R * new_T[k])
+    dz = calc_dz(nlyr, new_p, new_rho, g)
+    return conc, new_rho, dz, new_p

@@ -27,7 +27,17 @@ EXPORTED = ("hd_version", "hd_last_error", "hd_context_create", "hd_context_dest
             "hd_context_set_chunk", "hd_context_set_timing", "hd_context_get_timing",
             "hd_context_reserve", "hd_solve", "hd_quadrature")
 
+# every symbol include/hdharp.h declares (harp-side steps around the solve)
+HARP_EXPORTED = ("hd_attenuate", "hd_band_optics", "hd_band_flux", "hd_heating_rate",
+                 "hd_spherical_flux_correction")
+HD_COORD_WAVELENGTH, HD_COORD_WAVENUMBER = 0, 1
+
 _dp = ctypes.c_void_p
+
+
+class HdAttenuator(ctypes.Structure):
+    _fields_ = [("nrow", ctypes.c_int), ("wavelength", _dp), ("kext", _dp), ("ssa", _dp),
+                ("species", ctypes.c_int)]
 
 
 class HdConfig(ctypes.Structure):
@@ -72,7 +82,15 @@ def load(path: str = LIB_PATH):
                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.hd_quadrature.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                   ctypes.POINTER(ctypes.c_double)]
-    for name in EXPORTED:
+    ci, cd = ctypes.c_int, ctypes.c_double
+    lib.hd_attenuate.argtypes = [ctypes.POINTER(HdAttenuator), _dp, ci, ci, _dp, ci, ci, ci, _dp,
+                                 _dp]
+    lib.hd_band_optics.argtypes = [ctypes.POINTER(HdAttenuator), ci, _dp, ci, ci, _dp, ci, ci, ci,
+                                   _dp, ci, _dp, _dp]
+    lib.hd_band_flux.argtypes = [_dp, _dp, ci, ci, ci, _dp, _dp]
+    lib.hd_heating_rate.argtypes = [_dp, _dp, _dp, cd, ci, ci, _dp, _dp]
+    lib.hd_spherical_flux_correction.argtypes = [_dp, _dp, _dp, _dp, ci, ci, _dp]
+    for name in EXPORTED + HARP_EXPORTED:
         getattr(lib, name)
     _lib = lib
     return lib

@@ -126,16 +126,21 @@ int ensure_tables(hd_context* ctx) {
 }
 
 long auto_chunk(long nsolve, int nn, int nlyr, bool planck) {
-  // Enough solves per chunk to fill 256 CUs (one lane per solve in the NN <= 8
-  // sweep, one 16-lane team per solve above), bounded so the scratch stays
-  // within a fixed HBM budget (the rest of the 288 GB stays the caller's).
-  const double budget = 8.0 * 1024.0 * 1024.0 * 1024.0;  // bytes of scratch per chunk
-  const double per = 8.0 * (double)hd::scratch_doubles_per_solve(nn, nlyr, planck);
-  const long floor_n = nn <= hd::kMaxRegNN ? 65536 : 16384;
-  const long cap = std::max<long>(floor_n, (long)(budget / per));
-  const long target = std::min<long>(cap, 262144);
+  // NN <= 8: the sweep runs one lane per solve at one wave per SIMD (its
+  // register file is full), so a chunk of 65 536 solves is one wave on each of
+  // the 1024 SIMDs; more would leave a tail wave on a few of them.
+  // NN > 8: one 16-lane team per solve; chunks bounded by a scratch budget
+  // (the rest of the 288 GB stays the caller's).
+  long target;
+  if (nn <= hd::kMaxRegNN) {
+    target = 65536;
+  } else {
+    const double budget = 8.0 * 1024.0 * 1024.0 * 1024.0;  // bytes of scratch per chunk
+    const double per = 8.0 * (double)hd::scratch_doubles_per_solve(nn, nlyr, planck);
+    target = std::min<long>(262144, std::max<long>(16384, (long)(budget / per)));
+  }
   if (nsolve <= target) return nsolve;
-  long n = (nsolve + target - 1) / target;
+  const long n = (nsolve + target - 1) / target;
   return (nsolve + n - 1) / n;
 }
 
@@ -204,6 +209,19 @@ int validate(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, const d
 }
 
 }  // namespace
+
+namespace hd {
+int set_global_error(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  g_err = buf;
+  return code;
+}
+}  // namespace hd
 
 extern "C" {
 

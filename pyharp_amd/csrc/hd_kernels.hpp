@@ -105,6 +105,8 @@ hipError_t launch_solve_chunk_team(int nn, const PlanckArgs* pa, const TaucArgs*
                                    const LayerArgs& la, const SweepArgs& sa, hipStream_t stream,
                                    hipEvent_t* ev);
 size_t scratch_doubles_per_solve(int nn, int nlyr, bool planck);
+// record an error for hd_last_error(NULL) (entry points without a context); returns code
+int set_global_error(int code, const char* fmt, ...);
 // doubles per (layer, solve) of the layer-operator and back-substitution records
 size_t layer_record_doubles(int nn);
 size_t bsub_record_doubles(int nn);

@@ -1,9 +1,9 @@
 """The N>1 path on CPU: spectral sharding + one all-reduce of the band flux.
 
 Two gloo ranks each solve their own g-points (with the CPU oracle standing in
-for the device solve -- test infrastructure only) and complete the band flux
-with pyharp_amd.spectral.allreduce_band_flux; the result must equal the
-single-process band sum.
+for the device solve and the device band sum -- test infrastructure only) and
+complete the band flux with pyharp_amd.spectral.allreduce_band_flux; the
+result must equal the single-process band sum.
 """
 
 import os
@@ -41,11 +41,12 @@ def _worker(rank, world, port, out_path):
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import oracle_c
-    from pyharp_amd.spectral import allreduce_band_flux, band_flux, shard_gpoints
+    from pyharp_amd.spectral import allreduce_band_flux, shard_gpoints
     prop, bc, w, nstr = _problem()
     mine = shard_gpoints(prop.shape[0], world, rank)
     flux = oracle_c.forward(prop[mine], {k: v[mine] for k, v in bc.items()}, nstr=nstr)
-    part = band_flux(torch.as_tensor(flux), torch.as_tensor(w[mine]))
+    # the rank's partial band sum (on the GPU: hd_band_flux; here the test's own)
+    part = torch.as_tensor(np.einsum("g,gcld->cld", w[mine], flux))
     allreduce_band_flux(part)
     if rank == 0:
         np.save(out_path, part.numpy())

@@ -1,0 +1,130 @@
+"""HIP parity of the harp-side steps (include/hdharp.h) and the amars_sw case
+end to end, against oracle/harp_np.py + the C DISORT oracle.
+
+Tolerances: the optics and epilogue kernels do the reference's arithmetic in
+the reference's order, so they are held to 1e-13 relative (interpolation /
+sums in f64); fluxes to the north-star bound 1e-6 (tests/helpers.py); heating
+rates, being differences of fluxes, to 1e-6 of the column's largest |dT/dt|.
+"""
+
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import TOL, rel_err
+from oracle import harp_np as H
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+DATA = os.path.join(HERE, "golden", "data")
+DEV = torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _resources():
+    from pyharp_amd.opacity import add_resource_directory
+    add_resource_directory(DATA)
+
+
+def _attenuators():
+    from pyharp_amd.opacity import AttenuatorOptions, H2SO4Simple, S8Fuller
+    op = AttenuatorOptions().species_names(["S8", "H2SO4"]).species_weights([256.e-3, 98.e-3])
+    s8 = S8Fuller(op.copy().species_ids([0]).opacity_files(["s8_k_fuller.txt"]))
+    h2 = H2SO4Simple(op.copy().species_ids([1]).opacity_files(["h2so4.txt"]))
+    return s8, h2
+
+
+def _oracle_tables():
+    s8 = H.load_attenuator(os.path.join(DATA, "s8_k_fuller.txt"), 256e-3)
+    h2 = H.load_attenuator(os.path.join(DATA, "h2so4.txt"), 98e-3)
+    return [(s8[0], s8[1], 0), (h2[0], h2[1], 1)]
+
+
+def test_attenuator_forward_matches_oracle():
+    s8, h2 = _attenuators()
+    tabs = _oracle_tables()
+    rng = np.random.default_rng(5)
+    conc = rng.uniform(0, 1e-5, (3, 7, 2))
+    # wavenumbers inside, at and beyond both table ends
+    wave = np.r_[np.linspace(2000.0, 50000.0, 97), 1e4 / tabs[0][0][0], 1e4 / tabs[1][0][-1],
+                 100.0, 1e6]
+    for att, (kw, kd, sp) in zip((s8, h2), tabs):
+        got = att.forward(torch.as_tensor(conc, device=DEV),
+                          {"wavenumber": torch.as_tensor(wave, device=DEV)}).cpu().numpy()
+        ref = H.attenuate(kw, kd, sp, conc, wavenumber=wave)
+        np.testing.assert_allclose(got, ref, rtol=1e-13, atol=0)
+    # wavelength coordinate
+    wl = np.linspace(0.1, 6.0, 33)
+    got = s8.forward(torch.as_tensor(conc, device=DEV),
+                     {"wavelength": torch.as_tensor(wl, device=DEV)}).cpu().numpy()
+    ref = H.attenuate(tabs[0][0], tabs[0][1], 0, conc, wavelength=wl)
+    np.testing.assert_allclose(got, ref, rtol=1e-13, atol=0)
+
+
+@pytest.mark.parametrize("nprop", [2, 10])
+def test_band_optics_matches_oracle(nprop):
+    from pyharp_amd.opacity import band_optics
+    conc, rho, dz, p = H.amars_sw_atmosphere(os.path.join(DATA, "aerosol_output_data.txt"))
+    conc = np.repeat(conc, 3, axis=0) * np.array([1.0, 0.5, 0.0])[:, None, None]  # 3 columns
+    wave = H.short_wavenumber_grid(500)
+    got = band_optics(list(_attenuators()), torch.as_tensor(conc, device=DEV),
+                      torch.as_tensor(dz, device=DEV),
+                      {"wavenumber": torch.as_tensor(wave, device=DEV)}, nprop=nprop)
+    ref = H.band_optics(_oracle_tables(), conc, dz, nprop=nprop, wavenumber=wave)
+    np.testing.assert_allclose(got.cpu().numpy(), ref, rtol=1e-13, atol=0)
+    assert np.all(got[:, 2].cpu().numpy() == 0.0)  # empty column: tau 0, ssa 0 (not NaN)
+
+
+def test_band_flux_heating_spherical_match_oracle():
+    from pyharp_amd.spectral import band_flux, heating_rate, spherical_flux_correction
+    rng = np.random.default_rng(6)
+    G, C, L = 37, 5, 24
+    flux = rng.uniform(0, 100, (G, C, L + 1, 2))
+    w = rng.uniform(0, 1, G)
+    b = band_flux(torch.as_tensor(flux, device=DEV), torch.as_tensor(w, device=DEV))
+    bref = H.band_flux(flux, w)
+    np.testing.assert_allclose(b.cpu().numpy(), bref, rtol=1e-13)
+    dz = rng.uniform(100, 2000, (C, L))
+    rho = rng.uniform(0.01, 1.5, (C, L))
+    h = heating_rate(b, torch.as_tensor(dz, device=DEV), torch.as_tensor(rho, device=DEV), 844.0)
+    np.testing.assert_allclose(h.cpu().numpy(), H.heating_rate(bref, dz, rho, 844.0),
+                               rtol=1e-9, atol=1e-12 * np.abs(H.heating_rate(bref, dz, rho,
+                                                                             844.0)).max())
+    x1f = 6.4e6 + np.cumsum(np.r_[0.0, rng.uniform(1e3, 2e3, L)])
+    area = 4 * np.pi * x1f ** 2
+    vol = 4 / 3 * np.pi * np.diff(x1f ** 3)
+    sref = H.spherical_flux_correction(b.cpu().numpy(), x1f, area, vol)
+    spherical_flux_correction(b, torch.as_tensor(x1f, device=DEV),
+                              torch.as_tensor(area, device=DEV), torch.as_tensor(vol, device=DEV))
+    np.testing.assert_allclose(b.cpu().numpy(), sref, rtol=1e-12)
+
+
+@pytest.mark.parametrize("nstr", [8, 16])
+def test_amars_sw_end_to_end(oracle_c, nstr):
+    """examples/amars_sw.py (all on the GPU) vs the oracle pipeline on the same
+    atmosphere: prop, per-bin fluxes, band flux and heating rates."""
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "examples"))
+    import amars_sw
+    r = amars_sw.run(nstr=nstr, nwave=500, nlyr=40)
+    conc, rho, dz, p = H.amars_sw_atmosphere(os.path.join(DATA, "aerosol_output_data.txt"))
+    np.testing.assert_allclose(r["conc"], conc, rtol=1e-12)
+    np.testing.assert_allclose(r["dz"], dz, rtol=1e-12)
+    wave = H.short_wavenumber_grid(500)
+    prop = H.band_optics(_oracle_tables(), conc, dz, wavenumber=wave)
+    np.testing.assert_allclose(r["prop"].cpu().numpy(), prop, rtol=1e-11)
+    bc = {"fbeam": H.bb_toa_flux(wave, 1, 5772.0, 0.7), "umu0": np.ones((500, 1)),
+          "albedo": np.ones((500, 1))}
+    fref = oracle_c.forward(r["prop"].cpu().numpy(), bc, nstr=nstr, nmom=nstr)
+    f = r["flux"].cpu().numpy()
+    assert rel_err(f, fref).max() < TOL
+    bref = H.band_flux(fref, np.full(500, wave[1] - wave[0]))
+    assert rel_err(r["bflux"].cpu().numpy()[None], bref[None]).max() < TOL
+    href = H.heating_rate(bref, dz, rho, 844.0)
+    h = r["dTdt"].cpu().numpy()
+    assert np.abs(h - href).max() <= 1e-6 * np.abs(href).max()
+    # the example's own statement (amars_sw.cpp:75-77): TOA down within 2 W/m^2 of 410
+    assert abs(r["bflux"][0, -1, 1].item() - 410.0) < 2.0

@@ -16,8 +16,8 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _declared_functions():
-    with open(os.path.join(ROOT, "include", "hdisort.h")) as f:
+def _declared_functions(header="hdisort.h"):
+    with open(os.path.join(ROOT, "include", header)) as f:
         src = f.read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(hd_[a-z_]+)\s*\(", src)))
@@ -37,6 +37,22 @@ def test_exports_every_declared_symbol(lib):
     for name in names:
         assert hasattr(lib, name), name
     assert set(names) == set(_lib.EXPORTED)
+
+
+def test_exports_every_harp_symbol(lib):
+    from pyharp_amd import _lib
+    names = _declared_functions("hdharp.h")
+    assert set(names) == set(_lib.HARP_EXPORTED)
+    for name in names:
+        assert hasattr(lib, name), name
+
+
+def test_harp_ops_refuse_cpu_tensors():
+    from pyharp_amd.spectral import band_flux, heating_rate
+    with pytest.raises(RuntimeError, match="device"):
+        band_flux(torch.zeros((2, 1, 3, 2), dtype=torch.float64), torch.ones(2))
+    with pytest.raises(RuntimeError, match="device"):
+        heating_rate(torch.zeros((1, 3, 2), dtype=torch.float64), torch.ones(2), torch.ones(2), 1.0)
 
 
 def test_version(lib):
