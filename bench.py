@@ -68,7 +68,33 @@ CONFIGS = {
                umu0=(0.05, 1.0), label="C4 GCM batch"),
     "c5": dict(ncol=1000, ngpoint=64, nstr=32, nlyr=80, ssa=(0.9, 0.9999), g=(0.6, 0.9),
                umu0=(0.1, 1.0), label="C5 high-scatter aerosol"),
+    # thermal, non-scattering (SURVEY 8(d) C1 amars_lw ck and C3 line-by-line)
+    "c1": dict(ncol=1, ngpoint=16, nstr=8, nlyr=40, lw=True, tau=(1e-4, 20.0), band=(1.0, 150.0),
+               label="C1 amars_lw ck (synthetic k)"),
+    "c3": dict(ncol=1, ngpoint=19990, nstr=8, nlyr=40, lw=True, tau=(1e-5, 5.0),
+               band=(1.0, 2000.0), label="C3 line-by-line (synthetic k)"),
 }
+
+
+def make_lw_inputs(gpoints, ngpoint, ncol, nlyr, nstr, band, tau, dev, seed=20250217):
+    """Thermal, omega = 0: tau log-uniform, T linear 250 -> 150 K
+    bottom -> top, temf = layer2level (4th order), albedo 0 (even g) / 1 (odd g),
+    btemp = T_surface, spectral bins tiling `band` (ck: every g spans the band)."""
+    f64 = torch.float64
+    W = len(gpoints)
+    prop = torch.zeros((W, ncol, nlyr, 2 + nstr), dtype=f64, device=dev)
+    for i, g in enumerate(gpoints):
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(seed * 1000 + int(g))
+        u = torch.rand((ncol, nlyr), generator=gen, dtype=f64, device=dev)
+        prop[i, ..., 0] = 10.0 ** (np.log10(tau[0]) + u * np.log10(tau[1] / tau[0]))
+    tl = torch.linspace(250.0, 150.0, nlyr, dtype=f64, device=dev)[None, :].expand(ncol, nlyr)
+    from pyharp_amd import layer2level
+    temf = layer2level(tl.contiguous())
+    alb = torch.tensor([float(g % 2) for g in gpoints], dtype=f64, device=dev)
+    bc = {"albedo": alb[:, None].expand(W, ncol).contiguous(),
+          "btemp": temf[:, 0][None, :].expand(W, ncol).contiguous()}
+    return prop, bc, temf
 
 
 def make_inputs(gpoints, ncol, nlyr, nstr, planck, dev, seed=20250217, ssa=(0.0, 0.99),
@@ -113,9 +139,14 @@ def gpoint_weights(ngpoint):
     return w / w.sum()
 
 
-def wave_bounds(ngpoint):
-    lo = 10.0 + 30.0 * np.arange(ngpoint, dtype=np.float64)
-    return lo, lo + 30.0
+def wave_bounds(ngpoint, band=None, ck=False):
+    if band is None:
+        lo = 10.0 + 30.0 * np.arange(ngpoint, dtype=np.float64)
+        return lo, lo + 30.0
+    if ck:  # correlated-k: every g-point spans the whole band (amars_lw.cpp:23-31)
+        return np.full(ngpoint, band[0]), np.full(ngpoint, band[1])
+    edges = np.linspace(band[0], band[1], ngpoint + 1)
+    return edges[:-1].copy(), edges[1:].copy()
 
 
 def load_pmc(nstr: int, nlyr: int, planck: bool):
@@ -196,10 +227,17 @@ def main():
     from pyharp_amd.spectral import allreduce_band_flux, band_flux, shard_gpoints
     gpoints = shard_gpoints(G, world, rank)
     W = len(gpoints)
-    wl_all, wu_all = wave_bounds(G)
+    lw = cfgd.get("lw", False)
+    if lw:
+        args.planck = True
+    wl_all, wu_all = wave_bounds(G, cfgd.get("band"), ck=args.config == "c1")
     wl, wu = wl_all[gpoints], wu_all[gpoints]
-    prop, bc, temf = make_inputs(gpoints, ncol, nlyr, nstr, args.planck, dev,
-                                 ssa=cfgd["ssa"], gasym=cfgd["g"], umu0=cfgd["umu0"])
+    if lw:
+        prop, bc, temf = make_lw_inputs(gpoints, G, ncol, nlyr, nstr, cfgd["band"], cfgd["tau"],
+                                        dev)
+    else:
+        prop, bc, temf = make_inputs(gpoints, ncol, nlyr, nstr, args.planck, dev,
+                                     ssa=cfgd["ssa"], gasym=cfgd["g"], umu0=cfgd["umu0"])
     wts = torch.tensor(gpoint_weights(G)[gpoints], dtype=torch.float64, device=dev)
 
     op = DisortOptions().flags("lamber,quiet,onlyfl" + (",planck" if args.planck else ""))
@@ -244,7 +282,8 @@ def main():
     value = nsolve_total * args.steps / elapsed
     total_flop, k1_flop, k2_flop = algorithmic_flop(nstr, nlyr, args.planck)
     workload = (f"{cfgd['label']}: {ncol} columns x {G} g-points, nstr={nstr}, nmom={nstr}, "
-                f"nlyr={nlyr}, beam{' + planck' if args.planck else ''}")
+                f"nlyr={nlyr}, " + ("thermal (planck), omega=0" if lw else
+                                    f"beam{' + planck' if args.planck else ''}"))
 
     layer_kernel = "hd_layer_kernel" if nstr <= 16 else "hd_team_layer_kernel"
     if rank == 0:

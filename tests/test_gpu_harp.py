@@ -128,3 +128,22 @@ def test_amars_sw_end_to_end(oracle_c, nstr):
     assert np.abs(h - href).max() <= 1e-6 * np.abs(href).max()
     # the example's own statement (amars_sw.cpp:75-77): TOA down within 2 W/m^2 of 410
     assert abs(r["bflux"][0, -1, 1].item() - 410.0) < 2.0
+
+
+def test_amars_lw_example(oracle_c):
+    """examples/amars_lw.py: isothermal 300 K layers over an albedo-1 surface
+    (emissivity 0); per-g fluxes vs the oracle, no diffuse flux entering at the
+    top, and F_up = F_dn at the perfectly reflecting surface."""
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "examples"))
+    import amars_lw
+    r = amars_lw.run(nstr=8, ngpoint=16, nlyr=40)
+    prop = r["prop"].cpu().numpy()
+    temf = r["temf"].cpu().numpy()
+    bc = {"albedo": np.ones((16, 1)), "btemp": np.full((16, 1), 300.0)}
+    ref = oracle_c.forward(prop, bc, temf, nstr=8, planck=True, wave_lower=np.full(16, 1.0),
+                           wave_upper=np.full(16, 150.0))
+    f = r["flux"].cpu().numpy()
+    assert rel_err(f, ref).max() < TOL
+    assert np.all(np.abs(f[:, 0, -1, 1]) <= 1e-12 * np.abs(f).max())
+    np.testing.assert_allclose(f[:, 0, 0, 0], f[:, 0, 0, 1], rtol=1e-12)
+    assert r["bflux"].shape == (1, 41, 2)

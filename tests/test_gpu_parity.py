@@ -295,3 +295,41 @@ def test_cpp_dropin(oracle_c):
           "albedo": np.ones((nwave, ncol))}
     ref = oracle_c.forward(prop, bc, nstr=nstr)
     assert rel_err(got, ref).max() < TOL
+
+
+def _lw_problem(G, nstr, nlyr, tau, band, ck, seed=20250217):
+    """SURVEY 8(d) C1/C3 shapes (thermal, omega=0), host copy of bench.make_lw_inputs."""
+    rng = np.random.default_rng(seed)
+    prop = np.zeros((G, 1, nlyr, 2 + nstr))
+    prop[..., 0] = 10.0 ** rng.uniform(np.log10(tau[0]), np.log10(tau[1]), (G, 1, nlyr))
+    from oracle.disort_np import layer2level
+    temf = layer2level(np.linspace(250.0, 150.0, nlyr)[None, :])
+    bc = {"albedo": (np.arange(G) % 2).astype(float)[:, None],
+          "btemp": np.full((G, 1), temf[0, 0])}
+    if ck:
+        wl, wu = np.full(G, band[0]), np.full(G, band[1])
+    else:
+        e = np.linspace(band[0], band[1], G + 1)
+        wl, wu = e[:-1], e[1:]
+    return prop, bc, temf, wl, wu
+
+
+@pytest.mark.parametrize("nstr", [4, 8])
+def test_c1_amars_lw_shape(oracle_c, nstr):
+    """C1: 1 column, 16 g-points, nlyr=40, omega=0, Planck, albedo 0/1, nu in [1, 150]."""
+    prop, bc, temf, wl, wu = _lw_problem(16, nstr, 40, (1e-4, 20.0), (1.0, 150.0), ck=True)
+    d = _disort(nstr, 40, 16, 1, planck=True, wl=wl, wu=wu)
+    f = _run(d, prop, bc, temf)
+    ref = oracle_c.forward(prop, bc, temf, nstr=nstr, planck=True, wave_lower=wl, wave_upper=wu)
+    assert rel_err(f, ref).max() < TOL
+
+
+def test_c3_line_by_line_shape(oracle_c):
+    """C3: 1 column, 19 990 spectral bins of 0.1 cm^-1 tiling [1, 2000], nstr=8, nlyr=40,
+    omega=0, Planck -- every bin against the C oracle."""
+    G = 19990
+    prop, bc, temf, wl, wu = _lw_problem(G, 8, 40, (1e-5, 5.0), (1.0, 2000.0), ck=False)
+    d = _disort(8, 40, G, 1, planck=True, wl=wl, wu=wu)
+    f = _run(d, prop, bc, temf)
+    ref = oracle_c.forward(prop, bc, temf, nstr=8, planck=True, wave_lower=wl, wave_upper=wu)
+    assert rel_err(f, ref).max() < TOL
