@@ -205,26 +205,25 @@ __host__ __device__ constexpr bool round_has_pair(int m) {
   return false;
 }
 
-// One-sided (Hestenes) Jacobi on the columns of B: lane j holds column j of B
-// (b) and of V (vc).  Round M rotates the column pair (j, j^M) to make the two
-// orthogonal -- exactly the two-sided Jacobi rotation of B^T B for that pair,
-// built from column dot products -- so B^T B is never formed and no diagonal
-// has to be fished out of a lane-indexed register.  Both lanes of a pair form
-// their operands in the same order (products commute exactly), so the two
-// rotations agree bitwise.
-constexpr double kJacobiTol2 = 1.0e-30;  // (|b_p . b_q| / |b_p||b_q|)^2 threshold
+// One-sided (Hestenes) Jacobi on the columns of B: lane j holds column j of B.
+// Round M rotates the column pair (j, j^M) to make the two orthogonal --
+// exactly the two-sided Jacobi rotation of B^T B for that pair, built from
+// column dot products -- so B^T B is never formed and no diagonal has to be
+// fished out of a lane-indexed register.  Both lanes of a pair form their
+// operands in the same order (products commute exactly), so the two rotations
+// agree bitwise.  The rotations are not accumulated: with B = B0 V the
+// eigenvectors come out afterwards as V = B0^-1 B (two triangular solves, see
+// the layer kernel), which removes half of the cross-lane traffic per round.
+constexpr double kJacobiTol2 = 1.0e-30;  // rotate while (b_p.b_q)^2 > tol |b_p|^2 |b_q|^2
+constexpr double kJacobiLast2 = 1.0e-18;  // a sweep whose largest such ratio stayed below
+                                          // this leaves ~1e-18^2: the last one needed
 
 template <int NN, int M>
-__device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double (&vc)[NN], bool on,
-                                                  bool& rot_any) {
+__device__ __forceinline__ void team_jacobi_round(double (&b)[NN], bool on, double& r2max) {
   const int i = tlane();
   const int pi = i ^ M;
-  double bq[NN], vq[NN];
-  sfor<0, NN>([&](auto K) {
-    constexpr int k = HD_K(K);
-    bq[k] = xperm<M>(b[k]);
-    vq[k] = xperm<M>(vc[k]);
-  });
+  double bq[NN];
+  sfor<0, NN>([&](auto K) { bq[HD_K(K)] = xperm<M>(b[HD_K(K)]); });
   double own = 0.0, oth = 0.0, gam = 0.0;
   sfor<0, NN>([&](auto K) {
     constexpr int k = HD_K(K);
@@ -235,10 +234,13 @@ __device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double (&vc)[
   const bool lo = i < pi;
   const double app = lo ? own : oth;
   const double aqq = lo ? oth : own;
-  const bool r = on && i < NN && pi < NN && gam * gam > kJacobiTol2 * app * aqq;
+  const bool pair = i < NN && pi < NN;
+  const double g2 = gam * gam, pq = app * aqq;
+  const bool r = on && pair && g2 > kJacobiTol2 * pq;
+  if (pair) r2max = fmax(r2max, g2 * rcp_nr(pq > 0.0 ? pq : 1.0));
   // w = sqrt(d^2 + 4 g^2), u = |d| + w, z = 1/sqrt(2 w u): c = u z, s = sgn(d) 2 g z
   const double d = aqq - app;
-  const double w2 = r ? fma(d, d, 4.0 * gam * gam) : 1.0;
+  const double w2 = r ? fma(d, d, 4.0 * g2) : 1.0;
   const double w = w2 * rsq_nr(w2);
   const double u = fabs(d) + w;
   const double z = rsq_nr(2.0 * w * u);
@@ -246,28 +248,23 @@ __device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double (&vc)[
   const double c = r ? u * z : 1.0;
   const double s = r ? sg * gam * z : 0.0;
   const double se = lo ? -s : s;  // p side: c b_p - s b_q ; q side: s b_p + c b_q
-  sfor<0, NN>([&](auto K) {
-    constexpr int k = HD_K(K);
-    b[k] = fma(se, bq[k], c * b[k]);
-    vc[k] = fma(se, vq[k], c * vc[k]);
-  });
-  rot_any = rot_any || r;
+  sfor<0, NN>([&](auto K) { b[HD_K(K)] = fma(se, bq[HD_K(K)], c * b[HD_K(K)]); });
 }
 
-// Sweeps of rounds 1..15 until a sweep rotates nothing in any team of the wave
-// (a converged team keeps issuing no-op rotations) or max_sweeps.
+// Sweeps of rounds 1..15 until a sweep's largest rotation was small enough
+// that it was the last one needed (quadratic convergence), or max_sweeps.
+// A converged team issues no-op rotations while its wave-mates finish.
 template <int NN>
-__device__ __forceinline__ void team_jacobi(double (&b)[NN], double (&vc)[NN], int max_sweeps) {
-  const int i = tlane();
-  sfor<0, NN>([&](auto J) { vc[HD_K(J)] = i == HD_K(J) ? 1.0 : 0.0; });
+__device__ __forceinline__ void team_jacobi(double (&b)[NN], int max_sweeps) {
   bool on = true;
   for (int sweep = 0; sweep < max_sweeps; ++sweep) {
-    bool rot_any = false;
+    double r2max = 0.0;
     sfor<1, kTeam>([&](auto Mc) {
       constexpr int m = HD_K(Mc);
-      if constexpr (round_has_pair<NN>(m)) team_jacobi_round<NN, m>(b, vc, on, rot_any);
+      if constexpr (round_has_pair<NN>(m)) team_jacobi_round<NN, m>(b, on, r2max);
     });
-    on = bc<0>(team_sum(rot_any ? 1.0 : 0.0)) > 0.0;
+    // team max via the sum of indicator flags (uniform over the team)
+    on = bc<0>(team_sum(r2max > kJacobiLast2 ? 1.0 : 0.0)) > 0.0;
     if (__all(!on)) break;
   }
 }
@@ -413,11 +410,24 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_layer_kernel(LayerArgs A) 
       sfor<r, NN>([&](auto K) { t = fma(bc<HD_K(K)>(ap[r]), lt[HD_K(K)], t); });
       bcol[r] = t;
     });
-    team_jacobi<NN>(bcol, vt, A.max_sweeps);
+    team_jacobi<NN>(bcol, A.max_sweeps);
     double k2 = 0.0;
     sfor<0, NN>([&](auto K) { k2 = fma(bcol[HD_K(K)], bcol[HD_K(K)], k2); });
     if (act && !(k2 > 0.0)) st |= kStEigen;
     kk = act ? sqrt(k2 > 0.0 ? k2 : 0.0) : 0.0;
+    // v_j = B0^-1 b_j = L^-1 C^-T b_j (lane-local solves, matrix entries broadcast)
+    sfor_rev<0, NN>([&](auto I) {  // C^T y = b
+      constexpr int r = HD_K(I);
+      double t = bcol[r];
+      sfor<r + 1, NN>([&](auto K) { t = fma(-bc<HD_K(K)>(ap[r]), bcol[HD_K(K)], t); });
+      bcol[r] = t * bc<r>(rdc);
+    });
+    sfor<0, NN>([&](auto I) {  // L x = y
+      constexpr int r = HD_K(I);
+      double t = bcol[r];
+      sfor<0, r>([&](auto K) { t = fma(-bc<r>(lch[HD_K(K)]), vt[HD_K(K)], t); });
+      vt[r] = act ? t * bc<r>(rdl) : 0.0;
+    });
   }
   // v = rows of V (lane i: V_ij over j)
   double v[NN];
