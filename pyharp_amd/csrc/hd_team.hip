@@ -110,6 +110,17 @@ __device__ __forceinline__ double xperm(double x) {
   if constexpr (lo != 0) x = dpp<quad_xor(lo)>(x);
   return x;
 }
+// value held by team lane (i ^ M) through the LDS crossbar (ds_swizzle, bit
+// mode: and 0x1f, xor M inside each 32-lane half): no LDS storage, and the
+// exchange issues on the LDS pipe instead of the VALU the Jacobi rounds saturate
+template <int M>
+__device__ __forceinline__ double xswz(double x) {
+  static_assert(M > 0 && M < 16, "team XOR mask");
+  constexpr int pat = 0x1F | (M << 10);
+  const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(x), pat);
+  const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(x), pat);
+  return __hiloint2double(hi, lo);
+}
 // sum over the 16 lanes of the team (every lane receives a sum; the
 // association differs per lane, so take bc<0>() where a uniform value matters)
 __device__ __forceinline__ double team_sum(double x) {
@@ -219,18 +230,15 @@ constexpr double kJacobiLast2 = 1.0e-18;  // a sweep whose largest such ratio st
                                           // this leaves ~1e-18^2: the last one needed
 
 template <int NN, int M>
-__device__ __forceinline__ void team_jacobi_round(double (&b)[NN], bool on, double& r2max) {
+__device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double& own, bool on,
+                                                  double& r2max) {
   const int i = tlane();
   const int pi = i ^ M;
   double bq[NN];
-  sfor<0, NN>([&](auto K) { bq[HD_K(K)] = xperm<M>(b[HD_K(K)]); });
-  double own = 0.0, oth = 0.0, gam = 0.0;
-  sfor<0, NN>([&](auto K) {
-    constexpr int k = HD_K(K);
-    own = fma(b[k], b[k], own);
-    oth = fma(bq[k], bq[k], oth);
-    gam = fma(b[k], bq[k], gam);
-  });
+  sfor<0, NN>([&](auto K) { bq[HD_K(K)] = xswz<M>(b[HD_K(K)]); });
+  const double oth = xswz<M>(own);  // |b_partner|^2, tracked by the partner
+  double gam = 0.0;
+  sfor<0, NN>([&](auto K) { gam = fma(b[HD_K(K)], bq[HD_K(K)], gam); });
   const bool lo = i < pi;
   const double app = lo ? own : oth;
   const double aqq = lo ? oth : own;
@@ -249,6 +257,9 @@ __device__ __forceinline__ void team_jacobi_round(double (&b)[NN], bool on, doub
   const double s = r ? sg * gam * z : 0.0;
   const double se = lo ? -s : s;  // p side: c b_p - s b_q ; q side: s b_p + c b_q
   sfor<0, NN>([&](auto K) { b[HD_K(K)] = fma(se, bq[HD_K(K)], c * b[HD_K(K)]); });
+  // rotated norms: |c b_p - s b_q|^2 and |s b_p + c b_q|^2
+  const double cc = c * c, ss2 = s * s, cs2 = 2.0 * c * s * gam;
+  own = lo ? fma(cc, app, fma(ss2, aqq, -cs2)) : fma(ss2, app, fma(cc, aqq, cs2));
 }
 
 // Sweeps of rounds 1..15 until a sweep's largest rotation was small enough
@@ -259,9 +270,11 @@ __device__ __forceinline__ void team_jacobi(double (&b)[NN], int max_sweeps) {
   bool on = true;
   for (int sweep = 0; sweep < max_sweeps; ++sweep) {
     double r2max = 0.0;
+    double own = 0.0;  // |b_j|^2, exact at the start of every sweep, then tracked
+    sfor<0, NN>([&](auto K) { own = fma(b[HD_K(K)], b[HD_K(K)], own); });
     sfor<1, kTeam>([&](auto Mc) {
       constexpr int m = HD_K(Mc);
-      if constexpr (round_has_pair<NN>(m)) team_jacobi_round<NN, m>(b, on, r2max);
+      if constexpr (round_has_pair<NN>(m)) team_jacobi_round<NN, m>(b, own, on, r2max);
     });
     // team max via the sum of indicator flags (uniform over the team)
     on = bc<0>(team_sum(r2max > kJacobiLast2 ? 1.0 : 0.0)) > 0.0;
