@@ -35,6 +35,11 @@ struct hd_context {
   bool tables = false;
   hd_timing times{};
   std::string err;
+  // register path: back-substitution of chunk k on `side`, beside chunk k+1's
+  // layer kernel (its 44-VGPR waves fit next to the layer kernel's on a SIMD)
+  hipStream_t side = nullptr;
+  hipEvent_t ev_sweep[2] = {nullptr, nullptr};
+  hipEvent_t ev_back[2] = {nullptr, nullptr};
 };
 
 namespace {
@@ -250,6 +255,11 @@ int hd_context_create(hd_context** out, int device) {
   ctx->device = device;
   HD_HIP(ctx, hipSetDevice(device));
   HD_HIP(ctx, hipMalloc(&ctx->anyerr, sizeof(int)));
+  HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+  for (int b = 0; b < 2; ++b) {
+    HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_sweep[b], hipEventDisableTiming));
+    HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_back[b], hipEventDisableTiming));
+  }
   *out = ctx;
   return HD_OK;
 }
@@ -260,6 +270,11 @@ int hd_context_destroy(hd_context* ctx) {
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->status) (void)hipFree(ctx->status);
   if (ctx->anyerr) (void)hipFree(ctx->anyerr);
+  for (int b = 0; b < 2; ++b) {
+    if (ctx->ev_sweep[b]) (void)hipEventDestroy(ctx->ev_sweep[b]);
+    if (ctx->ev_back[b]) (void)hipEventDestroy(ctx->ev_back[b]);
+  }
+  if (ctx->side) (void)hipStreamDestroy(ctx->side);
   for (auto& e : ctx->pool)
     if (e) (void)hipEventDestroy(e);
   delete ctx;
@@ -344,12 +359,22 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
   HD_HIP(ctx, hipMemsetAsync(ctx->anyerr, 0, sizeof(int), stream));
   const int nm = std::max(0, std::min(cfg->nmom, cfg->nprop - 2));
 
-  for (long s0 = 0; s0 < nsolve; s0 += chunk) {
+  const bool reg = nn <= hd::kMaxRegNN;
+  long k = 0;  // chunk index
+  for (long s0 = 0; s0 < nsolve; s0 += chunk, ++k) {
     const int nsc = (int)std::min(chunk, nsolve - s0);
+    // scratch: layer ops | bsub[0] | planck | tauc | xsurf[0] | (register path:) bsub[1] | xsurf[1]
+    const int buf = reg ? (int)(k & 1) : 0;
     double* layer_ops = ctx->scratch;
-    double* bsub = layer_ops + ne1 * nlyr * (size_t)nsc;
-    double* planckv = planck ? bsub + ne2 * nlyr * (size_t)nsc : nullptr;
-    double* taucv = bsub + ne2 * nlyr * (size_t)nsc + (planck ? (size_t)(nlyr + 3) * nsc : 0);
+    double* bsub0 = layer_ops + ne1 * nlyr * (size_t)nsc;
+    double* planckv = planck ? bsub0 + ne2 * nlyr * (size_t)nsc : nullptr;
+    double* taucv = bsub0 + ne2 * nlyr * (size_t)nsc + (planck ? (size_t)(nlyr + 3) * nsc : 0);
+    double* xsurf0 = taucv + (size_t)nlyr * nsc;
+    double* bsub1 = xsurf0 + nsc;
+    double* xsurf1 = bsub1 + ne2 * nlyr * (size_t)nsc;
+    double* bsub = buf ? bsub1 : bsub0;
+    double* xsurf = buf ? xsurf1 : xsurf0;
+    if (reg && k >= 2) HD_HIP(ctx, hipStreamWaitEvent(stream, ctx->ev_back[buf], 0));
     hd::TaucArgs ta{};
     ta.prop = in->prop;
     ta.out = taucv;
@@ -391,6 +416,7 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
     hd::SweepArgs sa{};
     sa.scr = layer_ops;
     sa.bsub = bsub;
+    sa.xsurf = xsurf;
     sa.flux = flux;
     sa.fbeam = in->fbeam;
     sa.umu0 = in->umu0;
@@ -425,6 +451,19 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
                        : hd::launch_solve_chunk_team(nn, planck ? &pa : nullptr,
                                                      beam ? &ta : nullptr, la, sa, stream, ev);
     if (e != hipSuccess) return fail(ctx, HD_EHIP, "hd_solve: launch failed: %s", hipGetErrorString(e));
+    if (reg) {
+      HD_HIP(ctx, hipEventRecord(ctx->ev_sweep[buf], stream));
+      HD_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_sweep[buf], 0));
+      e = hd::launch_backsub_nn(nn, sa, ctx->side);
+      if (e != hipSuccess)
+        return fail(ctx, HD_EHIP, "hd_solve: back-substitution launch failed: %s",
+                    hipGetErrorString(e));
+      HD_HIP(ctx, hipEventRecord(ctx->ev_back[buf], ctx->side));
+    }
+  }
+  if (reg) {  // the caller's stream sees every chunk's fluxes complete
+    for (long b = 0; b < std::min<long>(k, 2); ++b)
+      HD_HIP(ctx, hipStreamWaitEvent(stream, ctx->ev_back[b], 0));
   }
   if (sync) {
     int any = 0;

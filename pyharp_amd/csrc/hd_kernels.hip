@@ -722,7 +722,36 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
     fo[1] = twopi * dn + dirsurf;
     chk += fo[0] + fo[1];
   }
-  // ---- back-substitution bottom -> top ----
+  A.xsurf[sl] = x;
+  if (!isfinite(chk)) st |= kStNonFinite;
+  if (st) {
+    atomicOr(&A.status[s], st);
+    if (st & 0x0F) atomicOr(A.anyerr, 1);
+  }
+}
+
+// ============================================================================
+// K3: per-solve back-substitution bottom -> top.  Split from the adding sweep
+// so that it runs at the occupancy of its own small register footprint (the
+// sweep's register file allows one wave per SIMD): a pure stream over the
+// back-substitution records, I+_top = t + ZT I+_bottom, fluxes per level.
+// ============================================================================
+template <int NN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
+void hd_backsub_kernel(SweepArgs A) {
+  const Quad<NN>& Qc = quad<NN>();
+  const long sl = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (sl >= A.nsc) return;
+  const long s = A.s0 + sl;
+  const int L = A.nlyr;
+  const size_t nsc = A.nsc;
+  const double twopi = 2.0 * kPi;
+  const double x = A.xsurf[sl];
+  double ip[NN];
+#pragma unroll
+  for (int i = 0; i < NN; ++i) ip[i] = Qc.g[i] * x;
+  double* fo = A.flux + (size_t)s * (L + 1) * 2;
+  double chk = 0.0;
   for (int lc = L - 1; lc >= 0; --lc) {
     const double* bp = A.bsub + (size_t)lc * ne2<NN>() * nsc + sl;
     double nip[NN];
@@ -745,10 +774,9 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
     fo[2 * lev + 1] = dn;
     chk += fo[2 * lev] + fo[2 * lev + 1];
   }
-  if (!isfinite(chk)) st |= kStNonFinite;
-  if (st) {
-    atomicOr(&A.status[s], st);
-    if (st & 0x0F) atomicOr(A.anyerr, 1);
+  if (!isfinite(chk)) {
+    atomicOr(&A.status[s], kStNonFinite);
+    atomicOr(A.anyerr, 1);
   }
 }
 
@@ -808,6 +836,27 @@ static hipError_t launch_chunk(const PlanckArgs* pa, const TaucArgs* ta, const L
   return hipGetLastError();
 }
 
+template <int NN>
+static void launch_backsub(const SweepArgs& sa, hipStream_t stream) {
+  hipLaunchKernelGGL(hd_backsub_kernel<NN>, dim3((unsigned)((sa.nsc + 255) / 256)), dim3(256), 0,
+                     stream, sa);
+}
+
+hipError_t launch_backsub_nn(int nn, const SweepArgs& sa, hipStream_t stream) {
+  switch (nn) {
+    case 1: launch_backsub<1>(sa, stream); break;
+    case 2: launch_backsub<2>(sa, stream); break;
+    case 3: launch_backsub<3>(sa, stream); break;
+    case 4: launch_backsub<4>(sa, stream); break;
+    case 5: launch_backsub<5>(sa, stream); break;
+    case 6: launch_backsub<6>(sa, stream); break;
+    case 7: launch_backsub<7>(sa, stream); break;
+    case 8: launch_backsub<8>(sa, stream); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_solve_chunk_nn(int nn, const PlanckArgs* pa, const TaucArgs* ta,
                                  const LayerArgs& la, const SweepArgs& sa, hipStream_t stream,
                                  hipEvent_t* ev) {
@@ -835,7 +884,10 @@ size_t bsub_record_doubles(int nn) {
 }
 
 size_t scratch_doubles_per_solve(int nn, int nlyr, bool planck) {
-  return (layer_record_doubles(nn) + bsub_record_doubles(nn)) * nlyr +
+  // register path: back-substitution records and xsurf double-buffered (the
+  // back-substitution of chunk k runs on a side stream beside chunk k+1)
+  const size_t nb = nn <= kMaxRegNN ? 2 : 1;
+  return layer_record_doubles(nn) * nlyr + nb * (bsub_record_doubles(nn) * nlyr + 1) +
          (planck ? (size_t)nlyr + 3 : 0) + (size_t)nlyr;  // + tauc
 }
 

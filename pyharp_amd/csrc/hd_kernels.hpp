@@ -72,6 +72,7 @@ struct LayerArgs {
 struct SweepArgs {
   const double* scr;
   double* bsub;
+  double* xsurf;  // [nsc] Lambert-surface amplitude x (I+ = g x), down -> up kernel
   double* flux;
   const double* fbeam;
   const double* umu0;
@@ -101,6 +102,8 @@ void launch_prologue(const PlanckArgs* pa, const TaucArgs* ta, hipStream_t strea
 hipError_t launch_solve_chunk_nn(int nn, const PlanckArgs* pa, const TaucArgs* ta,
                                  const LayerArgs& la, const SweepArgs& sa, hipStream_t stream,
                                  hipEvent_t* ev);
+// back-substitution of a register-path chunk (reads sa.bsub / sa.xsurf)
+hipError_t launch_backsub_nn(int nn, const SweepArgs& sa, hipStream_t stream);
 hipError_t launch_solve_chunk_team(int nn, const PlanckArgs* pa, const TaucArgs* ta,
                                    const LayerArgs& la, const SweepArgs& sa, hipStream_t stream,
                                    hipEvent_t* ev);
