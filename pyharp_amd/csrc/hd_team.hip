@@ -87,7 +87,7 @@ __device__ __forceinline__ int tlane() { return (int)(threadIdx.x & (kTeam - 1))
 
 template <int CTRL>
 __device__ __forceinline__ double dpp(double x) {
-  return __builtin_amdgcn_update_dpp(0.0, x, CTRL, 0xF, 0xF, false);
+  return __builtin_amdgcn_update_dpp(0.0, x, CTRL, 0xF, 0xF, true);  // every source lane valid
 }
 // value held by team lane K (row_newbcast:K)
 template <int K>
@@ -298,6 +298,7 @@ constexpr int ne2t() {
 // ============================================================================
 template <int NN>
 __global__ __launch_bounds__(kTeamBlock) void hd_team_layer_kernel(LayerArgs A) {
+  __shared__ double tr_lds[kTeamsPerBlock * kTeam * (kTeam + 1)];  // 16 transpose tiles
   constexpr int N = 2 * NN;
   const Quad<NN>& Qc = tquad<NN>();
   const int i = tlane();
@@ -442,16 +443,17 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_layer_kernel(LayerArgs A) 
       vt[r] = act ? t * bc<r>(rdl) : 0.0;
     });
   }
-  // v = rows of V (lane i: V_ij over j)
+  // v = rows of V (lane i: V_ij over j): transpose through this team's LDS
+  // tile (a team lives in one wave and LDS operations of a wave complete in
+  // order, so no barrier; the row stride kTeam+1 keeps both passes conflict-free)
   double v[NN];
-  sfor<0, NN>([&](auto J) {
-    constexpr int j = HD_K(J);
-    v[j] = 0.0;
-    sfor<0, NN>([&](auto I) {
-      const double x = bc<j>(vt[HD_K(I)]);
-      if (i == HD_K(I)) v[j] = x;
-    });
-  });
+  {
+    double* tile = tr_lds + (threadIdx.x >> 4) * (kTeam * (kTeam + 1));
+    sfor<0, NN>([&](auto I) { tile[HD_K(I) * (kTeam + 1) + i] = vt[HD_K(I)]; });
+    __builtin_amdgcn_wave_barrier();
+    sfor<0, NN>([&](auto J) { v[HD_K(J)] = act ? tile[i * (kTeam + 1) + HD_K(J)] : 0.0; });
+    __builtin_amdgcn_wave_barrier();
+  }
 
   // ---- beam particular solution Z+/- (c_upbeam) ----
   double zp = 0.0, zm = 0.0, e0 = 0.0;
