@@ -231,21 +231,26 @@ constexpr double kJacobiLast2 = 1.0e-18;  // a sweep whose largest such ratio st
 
 template <int NN, int M>
 __device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double& own, bool on,
-                                                  double& r2max) {
+                                                  bool& big) {
   const int i = tlane();
   const int pi = i ^ M;
   double bq[NN];
   sfor<0, NN>([&](auto K) { bq[HD_K(K)] = xswz<M>(b[HD_K(K)]); });
   const double oth = xswz<M>(own);  // |b_partner|^2, tracked by the partner
-  double gam = 0.0;
-  sfor<0, NN>([&](auto K) { gam = fma(b[HD_K(K)], bq[HD_K(K)], gam); });
+  double g0 = 0.0, g1 = 0.0;  // two chains: the partner columns arrive in order
+  sfor<0, NN>([&](auto K) {
+    constexpr int k = HD_K(K);
+    if constexpr (k % 2 == 0) g0 = fma(b[k], bq[k], g0);
+    else g1 = fma(b[k], bq[k], g1);
+  });
+  const double gam = g0 + g1;
   const bool lo = i < pi;
   const double app = lo ? own : oth;
   const double aqq = lo ? oth : own;
   const bool pair = i < NN && pi < NN;
   const double g2 = gam * gam, pq = app * aqq;
   const bool r = on && pair && g2 > kJacobiTol2 * pq;
-  if (pair) r2max = fmax(r2max, g2 * rcp_nr(pq > 0.0 ? pq : 1.0));
+  big = big || (pair && g2 > kJacobiLast2 * pq);
   // w = sqrt(d^2 + 4 g^2), u = |d| + w, z = 1/sqrt(2 w u): c = u z, s = sgn(d) 2 g z
   const double d = aqq - app;
   const double w2 = r ? fma(d, d, 4.0 * g2) : 1.0;
@@ -269,15 +274,15 @@ template <int NN>
 __device__ __forceinline__ void team_jacobi(double (&b)[NN], int max_sweeps) {
   bool on = true;
   for (int sweep = 0; sweep < max_sweeps; ++sweep) {
-    double r2max = 0.0;
+    bool big = false;  // some pair of this lane had (b_p.b_q)^2 > kJacobiLast2 |b_p|^2 |b_q|^2
     double own = 0.0;  // |b_j|^2, exact at the start of every sweep, then tracked
     sfor<0, NN>([&](auto K) { own = fma(b[HD_K(K)], b[HD_K(K)], own); });
     sfor<1, kTeam>([&](auto Mc) {
       constexpr int m = HD_K(Mc);
-      if constexpr (round_has_pair<NN>(m)) team_jacobi_round<NN, m>(b, own, on, r2max);
+      if constexpr (round_has_pair<NN>(m)) team_jacobi_round<NN, m>(b, own, on, big);
     });
     // team max via the sum of indicator flags (uniform over the team)
-    on = bc<0>(team_sum(r2max > kJacobiLast2 ? 1.0 : 0.0)) > 0.0;
+    on = bc<0>(team_sum(big ? 1.0 : 0.0)) > 0.0;
     if (__all(!on)) break;
   }
 }
