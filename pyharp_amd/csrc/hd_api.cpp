@@ -40,6 +40,7 @@ struct hd_context {
   hipStream_t side = nullptr;
   hipEvent_t ev_sweep[2] = {nullptr, nullptr};
   hipEvent_t ev_back[2] = {nullptr, nullptr};
+  hipEvent_t ev_pro[2] = {nullptr, nullptr};  // next chunk's prologue done (side stream)
 };
 
 namespace {
@@ -259,6 +260,7 @@ int hd_context_create(hd_context** out, int device) {
   for (int b = 0; b < 2; ++b) {
     HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_sweep[b], hipEventDisableTiming));
     HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_back[b], hipEventDisableTiming));
+    HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_pro[b], hipEventDisableTiming));
   }
   *out = ctx;
   return HD_OK;
@@ -273,6 +275,7 @@ int hd_context_destroy(hd_context* ctx) {
   for (int b = 0; b < 2; ++b) {
     if (ctx->ev_sweep[b]) (void)hipEventDestroy(ctx->ev_sweep[b]);
     if (ctx->ev_back[b]) (void)hipEventDestroy(ctx->ev_back[b]);
+    if (ctx->ev_pro[b]) (void)hipEventDestroy(ctx->ev_pro[b]);
   }
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   for (auto& e : ctx->pool)
@@ -360,48 +363,71 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
   const int nm = std::max(0, std::min(cfg->nmom, cfg->nprop - 2));
 
   const bool reg = nn <= hd::kMaxRegNN;
-  long k = 0;  // chunk index
-  for (long s0 = 0; s0 < nsolve; s0 += chunk, ++k) {
-    const int nsc = (int)std::min(chunk, nsolve - s0);
-    // scratch: layer ops | bsub[0] | planck | tauc | xsurf[0] | (register path:) bsub[1] | xsurf[1]
-    const int buf = reg ? (int)(k & 1) : 0;
-    double* layer_ops = ctx->scratch;
-    double* bsub0 = layer_ops + ne1 * nlyr * (size_t)nsc;
-    double* planckv = planck ? bsub0 + ne2 * nlyr * (size_t)nsc : nullptr;
-    double* taucv = bsub0 + ne2 * nlyr * (size_t)nsc + (planck ? (size_t)(nlyr + 3) * nsc : 0);
-    double* xsurf0 = taucv + (size_t)nlyr * nsc;
-    double* bsub1 = xsurf0 + nsc;
-    double* xsurf1 = bsub1 + ne2 * nlyr * (size_t)nsc;
-    double* bsub = buf ? bsub1 : bsub0;
-    double* xsurf = buf ? xsurf1 : xsurf0;
-    if (reg && k >= 2) HD_HIP(ctx, hipStreamWaitEvent(stream, ctx->ev_back[buf], 0));
-    hd::TaucArgs ta{};
+  const bool beam = in->fbeam != nullptr;
+  const int nb = reg ? 2 : 1;  // buffers of the per-chunk regions that live across chunks
+  // Scratch regions, sized for the largest chunk so that no region moves between
+  // chunks (inside a region the kernels interleave with the chunk's own nsc):
+  //   layer ops | bsub[nb] | xsurf[nb] | planck[nb] | tauc[nb]
+  // Register path: chunk k uses buffer k&1; its back-substitution (side stream)
+  // overlaps chunk k+1, whose tauc/planck prologue (side stream) overlaps chunk k.
+  double* layer_ops = ctx->scratch;
+  double* bsub_b[2];
+  double* xsurf_b[2];
+  double* planck_b[2];
+  double* tauc_b[2];
+  {
+    double* q = layer_ops + ne1 * nlyr * (size_t)chunk;
+    for (int b = 0; b < nb; ++b, q += ne2 * nlyr * (size_t)chunk) bsub_b[b] = q;
+    for (int b = 0; b < nb; ++b, q += chunk) xsurf_b[b] = q;
+    for (int b = 0; b < nb; ++b) {
+      planck_b[b] = planck ? q : nullptr;
+      if (planck) q += (size_t)(nlyr + 3) * chunk;
+    }
+    for (int b = 0; b < nb; ++b, q += (size_t)nlyr * chunk) tauc_b[b] = q;
+  }
+  auto prologue_args = [&](long s0, int nsc, int b, hd::TaucArgs& ta, hd::PlanckArgs& pa) {
+    ta = hd::TaucArgs{};
     ta.prop = in->prop;
-    ta.out = taucv;
+    ta.out = tauc_b[b];
     ta.s0 = s0;
     ta.nsc = nsc;
     ta.nlyr = nlyr;
     ta.nprop = cfg->nprop;
     ta.use_f = nm >= cfg->nstr;
     ta.f_slot = 1 + cfg->nstr;
-    hd::PlanckArgs pa{};
+    pa = hd::PlanckArgs{};
     pa.temf = in->temf;
     pa.btemp = in->btemp;
     pa.ttemp = in->ttemp;
     pa.temis = in->temis;
     pa.wlo = in->wave_lower;
     pa.whi = in->wave_upper;
-    pa.out = planckv;
+    pa.out = planck_b[b];
     pa.s0 = s0;
     pa.nsc = nsc;
     pa.ncol = in->ncol;
     pa.nlyr = nlyr;
+  };
+
+  long k = 0;  // chunk index
+  for (long s0 = 0; s0 < nsolve; s0 += chunk, ++k) {
+    const int nsc = (int)std::min(chunk, nsolve - s0);
+    const int buf = reg ? (int)(k & 1) : 0;
+    hd::TaucArgs ta;
+    hd::PlanckArgs pa;
+    prologue_args(s0, nsc, buf, ta, pa);
+    if (!reg || k == 0) {
+      hd::launch_prologue(planck ? &pa : nullptr, beam ? &ta : nullptr, stream);
+    } else {
+      HD_HIP(ctx, hipStreamWaitEvent(stream, ctx->ev_pro[buf], 0));
+    }
+    if (reg && k >= 2) HD_HIP(ctx, hipStreamWaitEvent(stream, ctx->ev_back[buf], 0));
     hd::LayerArgs la{};
     la.prop = in->prop;
-    la.tauc = taucv;
+    la.tauc = tauc_b[buf];
     la.fbeam = in->fbeam;
     la.umu0 = in->umu0;
-    la.planckv = planckv;
+    la.planckv = planck_b[buf];
     la.scr = layer_ops;
     la.status = status;
     la.anyerr = ctx->anyerr;
@@ -415,14 +441,14 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
     la.max_sweeps = 16;
     hd::SweepArgs sa{};
     sa.scr = layer_ops;
-    sa.bsub = bsub;
-    sa.xsurf = xsurf;
+    sa.bsub = bsub_b[buf];
+    sa.xsurf = xsurf_b[buf];
     sa.flux = flux;
     sa.fbeam = in->fbeam;
     sa.umu0 = in->umu0;
     sa.albedo = in->albedo;
     sa.fisot = in->fisot;
-    sa.planckv = planckv;
+    sa.planckv = planck_b[buf];
     sa.status = status;
     sa.anyerr = ctx->anyerr;
     sa.s0 = s0;
@@ -444,15 +470,21 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
       ev = &ctx->pool[ctx->pool_used];
       ctx->pool_used += 3;
     }
-    const bool beam = in->fbeam != nullptr;
-    hipError_t e = nn <= hd::kMaxRegNN
-                       ? hd::launch_solve_chunk_nn(nn, planck ? &pa : nullptr,
-                                                   beam ? &ta : nullptr, la, sa, stream, ev)
-                       : hd::launch_solve_chunk_team(nn, planck ? &pa : nullptr,
-                                                     beam ? &ta : nullptr, la, sa, stream, ev);
+    hipError_t e = reg ? hd::launch_solve_chunk_nn(nn, nullptr, nullptr, la, sa, stream, ev)
+                       : hd::launch_solve_chunk_team(nn, nullptr, nullptr, la, sa, stream, ev);
     if (e != hipSuccess) return fail(ctx, HD_EHIP, "hd_solve: launch failed: %s", hipGetErrorString(e));
     if (reg) {
       HD_HIP(ctx, hipEventRecord(ctx->ev_sweep[buf], stream));
+      // next chunk's prologue into the other buffer (free: the side stream already
+      // waited for the sweep of chunk k-1, the last user of that buffer)
+      const long s1 = s0 + chunk;
+      if (s1 < nsolve) {
+        hd::TaucArgs ta1;
+        hd::PlanckArgs pa1;
+        prologue_args(s1, (int)std::min(chunk, nsolve - s1), buf ^ 1, ta1, pa1);
+        hd::launch_prologue(planck ? &pa1 : nullptr, beam ? &ta1 : nullptr, ctx->side);
+        HD_HIP(ctx, hipEventRecord(ctx->ev_pro[buf ^ 1], ctx->side));
+      }
       HD_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_sweep[buf], 0));
       e = hd::launch_backsub_nn(nn, sa, ctx->side);
       if (e != hipSuccess)

@@ -884,11 +884,13 @@ size_t bsub_record_doubles(int nn) {
 }
 
 size_t scratch_doubles_per_solve(int nn, int nlyr, bool planck) {
-  // register path: back-substitution records and xsurf double-buffered (the
-  // back-substitution of chunk k runs on a side stream beside chunk k+1)
+  // register path: back-substitution records, xsurf and the tauc/planck
+  // prologue are double-buffered (chunk k's back-substitution and chunk k+1's
+  // prologue run on a side stream beside the main chain), see hd_solve
   const size_t nb = nn <= kMaxRegNN ? 2 : 1;
-  return layer_record_doubles(nn) * nlyr + nb * (bsub_record_doubles(nn) * nlyr + 1) +
-         (planck ? (size_t)nlyr + 3 : 0) + (size_t)nlyr;  // + tauc
+  return layer_record_doubles(nn) * nlyr +
+         nb * (bsub_record_doubles(nn) * nlyr + 1 + (planck ? (size_t)nlyr + 3 : 0) +
+               (size_t)nlyr);
 }
 
 }  // namespace hd
