@@ -254,9 +254,9 @@ __device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double& own, 
   // w = sqrt(d^2 + 4 g^2), u = |d| + w, z = 1/sqrt(2 w u): c = u z, s = sgn(d) 2 g z
   const double d = aqq - app;
   const double w2 = r ? fma(d, d, 4.0 * g2) : 1.0;
-  const double w = w2 * rsq_nr(w2);
+  const double w = w2 * rsq_nr1(w2);
   const double u = fabs(d) + w;
-  const double z = rsq_nr(2.0 * w * u);
+  const double z = rsq_nr1(2.0 * w * u);
   const double sg = d < 0.0 ? -2.0 : 2.0;
   const double c = r ? u * z : 1.0;
   const double s = r ? sg * gam * z : 0.0;
