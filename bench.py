@@ -212,12 +212,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # HD_BENCH_REHEARSE=1: rehearse the N>1 path on a box with fewer GPUs than
+    # ranks (ranks share devices, gloo instead of RCCL); never set by the driver
+    rehearse = os.environ.get("HD_BENCH_REHEARSE") == "1"
+    dev_index = local_rank % torch.cuda.device_count() if rehearse else local_rank
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev_index)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+    dev = torch.device("cuda", dev_index)
     torch.cuda.set_device(dev)
 
     from pyharp_amd import Disort, DisortOptions
@@ -241,7 +248,7 @@ def main():
     wts = torch.tensor(gpoint_weights(G)[gpoints], dtype=torch.float64, device=dev)
 
     op = DisortOptions().flags("lamber,quiet,onlyfl" + (",planck" if args.planck else ""))
-    op.nwave(W).ncol(ncol).device(local_rank)
+    op.nwave(W).ncol(ncol).device(dev_index)
     if args.planck:
         op.wave_lower(list(wl)).wave_upper(list(wu))
     op.ds().nlyr, op.ds().nstr, op.ds().nmom = nlyr, nstr, nstr
@@ -258,7 +265,7 @@ def main():
     torch.cuda.synchronize()
     if int((status & 0xF).any()):
         raise RuntimeError("bench: solver reported errors in the warm-up")
-    ctx = _context(local_rank)
+    ctx = _context(dev_index)
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
@@ -331,7 +338,8 @@ def main():
             "config": {"workload": workload, "ncol": ncol, "ngpoint": G, "nstr": nstr,
                        "nmom": nstr, "nlyr": nlyr, "planck": bool(args.planck),
                        "parallelism": f"spectral g mod {world}",
-                       "collective": "all_reduce of the g-weighted band flux (RCCL)" if world > 1
+                       "collective": ("all_reduce of the g-weighted band flux (" +
+                                      ("gloo, rehearsal" if rehearse else "RCCL") + ")") if world > 1
                        else "none"},
             "roofline": roofline, "path_roofline": whole, "cpu_baseline": cpu,
             "max_rel_err_vs_cpu_restatement": max_err,
