@@ -1,13 +1,18 @@
 #!/bin/bash
-# Compile the C++ drop-in check against the container's libtorch (ROCm build)
-# and the in-tree libhdisort.so.  Output: tests/cpp/disort_dropin
+# Compile the C++ drop-in checks against the container's libtorch (ROCm build)
+# and the in-tree libhdisort.so.  Outputs: tests/cpp/disort_dropin, tests/cpp/amars_sw_dropin
 set -euo pipefail
 HERE=$(cd "$(dirname "$0")" && pwd)
 ROOT=$(cd "$HERE/../.." && pwd)
 TORCH=$(python -c "import torch, os; print(os.path.dirname(torch.__file__))")
 ABI=$(python -c "import torch; print(int(torch._C._GLIBCXX_USE_CXX11_ABI))")
-/opt/rocm/bin/hipcc -O2 -std=c++17 -D_GLIBCXX_USE_CXX11_ABI=$ABI -D__HIP_PLATFORM_AMD__ -DUSE_ROCM \
-  -I"$ROOT/include" -I"$TORCH/include" -I"$TORCH/include/torch/csrc/api/include" \
-  "$HERE/disort_dropin.cpp" -o "$HERE/disort_dropin" \
-  -L"$TORCH/lib" -Wl,-rpath,"$TORCH/lib" -ltorch -ltorch_cpu -lc10 -ltorch_hip -lc10_hip \
-  -L"$ROOT/pyharp_amd" -Wl,-rpath,'$ORIGIN/../../pyharp_amd' -lhdisort
+build() {
+  /opt/rocm/bin/hipcc -O2 -std=c++17 -D_GLIBCXX_USE_CXX11_ABI=$ABI -D__HIP_PLATFORM_AMD__ -DUSE_ROCM \
+    -I"$ROOT/include" -I"$TORCH/include" -I"$TORCH/include/torch/csrc/api/include" \
+    "$HERE/$1.cpp" -o "$HERE/$1" \
+    -L"$TORCH/lib" -Wl,-rpath,"$TORCH/lib" -ltorch -ltorch_cpu -lc10 -ltorch_hip -lc10_hip \
+    -L"$ROOT/pyharp_amd" -Wl,-rpath,'$ORIGIN/../../pyharp_amd' -lhdisort
+}
+build disort_dropin &
+build amars_sw_dropin &
+wait %1 && wait %2

@@ -147,3 +147,29 @@ def test_amars_lw_example(oracle_c):
     assert np.all(np.abs(f[:, 0, -1, 1]) <= 1e-12 * np.abs(f).max())
     np.testing.assert_allclose(f[:, 0, 0, 0], f[:, 0, 0, 1], rtol=1e-12)
     assert r["bflux"].shape == (1, 41, 2)
+
+
+@pytest.mark.parametrize("nstr", [8, 16])
+def test_cpp_amars_sw(oracle_c, nstr):
+    """tests/cpp/amars_sw_dropin.cpp: the reference's amars_sw main() with the
+    harp_amd C++ modules (include/harp_amd/{opacity,spectral,disort}.hpp) --
+    band flux and heating rates vs the oracle pipeline."""
+    import subprocess
+    root = os.path.dirname(HERE)
+    exe = os.path.join(root, "tests", "cpp", "amars_sw_dropin")
+    if not os.path.exists(exe):
+        subprocess.run([os.path.join(root, "tests", "cpp", "build.sh")], check=True)
+    out = subprocess.run([exe, DATA, str(nstr)], check=True, capture_output=True,
+                         text=True).stdout.split("\n")
+    lev = np.array([[float(x) for x in l.split()[2:]] for l in out if l.startswith("level")])
+    lay = np.array([float(l.split()[2]) for l in out if l.startswith("layer")])
+    conc, rho, dz, p = H.amars_sw_atmosphere(os.path.join(DATA, "aerosol_output_data.txt"))
+    wave = H.short_wavenumber_grid(500)
+    prop = H.band_optics(_oracle_tables(), conc, dz, wavenumber=wave)
+    bc = {"fbeam": H.bb_toa_flux(wave, 1, 5772.0, 0.7), "umu0": np.ones((500, 1)),
+          "albedo": np.ones((500, 1))}
+    fref = oracle_c.forward(prop, bc, nstr=nstr, nmom=nstr)
+    bref = H.band_flux(fref, np.full(500, wave[1] - wave[0]))
+    assert rel_err(lev[None], bref).max() < TOL
+    href = H.heating_rate(bref, dz, rho, 844.0)[0]
+    assert np.abs(lay - href).max() <= 1e-6 * np.abs(href).max()
