@@ -203,6 +203,8 @@ def main():
     ap.add_argument("--nstr", type=int, default=None)
     ap.add_argument("--planck", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the solve + band sum as one captured HIP graph per step")
     args = ap.parse_args()
     cfgd = CONFIGS[args.config]
     for k in ("ncol", "ngpoint", "nlyr", "nstr"):
@@ -256,9 +258,30 @@ def main():
     flux = torch.empty((W, ncol, nlyr + 1, 2), dtype=torch.float64, device=dev)
     status = torch.zeros(W * ncol, dtype=torch.int32, device=dev)
 
-    def step():
+    band = torch.empty((ncol, nlyr + 1, 2), dtype=torch.float64, device=dev)
+
+    def solve():
         disort.forward(prop, bc, temf, status=status, out=flux)
-        return allreduce_band_flux(band_flux(flux, wts))
+        band_flux(flux, wts, out=band)
+
+    graph = None
+    if args.graph:
+        solve()  # sizes the context's scratch and tables before capture
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        cs = torch.cuda.Stream(device=dev)
+        cs.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(cs):
+            with torch.cuda.graph(graph, stream=cs):
+                solve()
+        torch.cuda.synchronize()
+
+    def step():
+        if graph is not None:
+            graph.replay()
+        else:
+            solve()
+        return allreduce_band_flux(band)
 
     for _ in range(args.warmup):
         step()
@@ -280,6 +303,18 @@ def main():
     elapsed = time.perf_counter() - t0
     tm = ctx.timing()
     ctx.set_timing(False)
+    timing_note = "HIP events on the solve stream over the timed steps"
+    if graph is not None:  # replays carry no timing events: one eager step for the kernels
+        torch.cuda.synchronize()
+        ctx.set_timing(True)
+        solve()
+        torch.cuda.synchronize()
+        tm = ctx.timing()
+        ctx.set_timing(False)
+        steps_timed = 1
+        timing_note = "HIP events on one eager step after the graph-replayed timed steps"
+    else:
+        steps_timed = args.steps
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -296,7 +331,7 @@ def main():
     if rank == 0:
         # dominant kernel roofline (the layer-setup kernel), per launch
         k1_avg_ms = tm.layer_ms / max(tm.layer_launches, 1)
-        solves_per_launch = W * ncol * args.steps / max(tm.layer_launches, 1)
+        solves_per_launch = W * ncol * steps_timed / max(tm.layer_launches, 1)
         ach = k1_flop * solves_per_launch / (k1_avg_ms * 1e-3) / 1e12
         pmc = load_pmc(nstr, nlyr, args.planck)
         traffic = None
@@ -319,8 +354,9 @@ def main():
                             "achieved uses the SURVEY 8(d) algorithmic FLOP convention"}
         whole = {"achieved_tflops": round(total_flop * value / 1e12, 3),
                  "frac": round(total_flop * value / 1e12 / FP64_PEAK_TFLOPS / world, 4),
-                 "layer_ms_per_step": round(tm.layer_ms / args.steps, 3),
-                 "sweep_ms_per_step": round(tm.sweep_ms / args.steps, 3)}
+                 "layer_ms_per_step": round(tm.layer_ms / steps_timed, 3),
+                 "sweep_ms_per_step": round(tm.sweep_ms / steps_timed, 3),
+                 "timing": timing_note}
         cpu = None
         max_err = None
         if world == 1 and not args.no_cpu_baseline:
@@ -338,6 +374,7 @@ def main():
             "config": {"workload": workload, "ncol": ncol, "ngpoint": G, "nstr": nstr,
                        "nmom": nstr, "nlyr": nlyr, "planck": bool(args.planck),
                        "parallelism": f"spectral g mod {world}",
+                       "hip_graph": bool(args.graph),
                        "collective": ("all_reduce of the g-weighted band flux (" +
                                       ("gloo, rehearsal" if rehearse else "RCCL") + ")") if world > 1
                        else "none"},

@@ -41,6 +41,7 @@ struct hd_context {
   hipEvent_t ev_sweep[2] = {nullptr, nullptr};
   hipEvent_t ev_back[2] = {nullptr, nullptr};
   hipEvent_t ev_pro[2] = {nullptr, nullptr};  // next chunk's prologue done (side stream)
+  hipEvent_t ev_fork = nullptr;                // start of a solve on the caller's stream
 };
 
 namespace {
@@ -257,6 +258,7 @@ int hd_context_create(hd_context** out, int device) {
   HD_HIP(ctx, hipSetDevice(device));
   HD_HIP(ctx, hipMalloc(&ctx->anyerr, sizeof(int)));
   HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+  HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
   for (int b = 0; b < 2; ++b) {
     HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_sweep[b], hipEventDisableTiming));
     HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_back[b], hipEventDisableTiming));
@@ -277,6 +279,7 @@ int hd_context_destroy(hd_context* ctx) {
     if (ctx->ev_back[b]) (void)hipEventDestroy(ctx->ev_back[b]);
     if (ctx->ev_pro[b]) (void)hipEventDestroy(ctx->ev_pro[b]);
   }
+  if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   for (auto& e : ctx->pool)
     if (e) (void)hipEventDestroy(e);
@@ -409,6 +412,12 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
     pa.nlyr = nlyr;
   };
 
+  if (reg) {
+    // fork: the side stream sees everything the caller's stream did before this
+    // call (the inputs) -- and, under stream capture, joins the graph here
+    HD_HIP(ctx, hipEventRecord(ctx->ev_fork, stream));
+    HD_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+  }
   long k = 0;  // chunk index
   for (long s0 = 0; s0 < nsolve; s0 += chunk, ++k) {
     const int nsc = (int)std::min(chunk, nsolve - s0);

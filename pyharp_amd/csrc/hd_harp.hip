@@ -13,7 +13,8 @@
 //                          ssa = sum ssa k c / sum k c, moments 0
 //                          [amars_sw.cpp:261-271]
 //   hd_band_flux_kernel    per (col, level, dir): sum_w weight_w F_w in w order
-//                          [amars_lw.cpp:84-88]
+//                          [amars_lw.cpp:84-88]; hd_band_flux_wave_kernel: a
+//                          wave per output when outputs are few and bins many
 //   hd_heating_kernel      per (col, layer)  [amars_sw.cpp:291-302]
 //   hd_spherical_kernel    per (col, dir): top-down recurrence
 //                          [spherical_flux_correction.cpp:3-17]
@@ -137,6 +138,21 @@ __global__ __launch_bounds__(256) void hd_band_flux_kernel(const double* flux,
   double s = 0.0;
   for (int w = 0; w < nwave; ++w) s = fma(weight[w], flux[(size_t)w * m + t], s);
   bflux[t] = s;
+}
+
+// few outputs, many bins (one column line-by-line: ~80 outputs x 2e4 bins): a
+// wave per output, lanes stride over w, fixed-order butterfly at the end
+__global__ __launch_bounds__(256) void hd_band_flux_wave_kernel(const double* flux,
+                                                                const double* weight, int nwave,
+                                                                long m, double* bflux) {
+  const long t = (long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (t >= m) return;  // whole wave
+  double s = 0.0;
+  for (int w = lane; w < nwave; w += 64) s = fma(weight[w], flux[(size_t)w * m + t], s);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) bflux[t] = s;
 }
 
 __global__ __launch_bounds__(256) void hd_heating_kernel(const double* bflux, const double* dz,
@@ -273,8 +289,13 @@ int hd_band_flux(const double* flux, const double* weight, int nwave, int ncol, 
   if ((nwave > 0 && (!flux || !weight)) || !bflux)
     return hd::set_global_error(HD_EINVAL, "hd_band_flux: null array");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream_);
-  hipLaunchKernelGGL(hd::hd_band_flux_kernel, dim3(nblk(m, 256)), dim3(256), 0, s, flux, weight,
-                     nwave, m, bflux);
+  if (m >= 65536 || nwave < 256) {  // a lane per output: coalesced, w in order
+    hipLaunchKernelGGL(hd::hd_band_flux_kernel, dim3(nblk(m, 256)), dim3(256), 0, s, flux,
+                       weight, nwave, m, bflux);
+  } else {  // a wave per output
+    hipLaunchKernelGGL(hd::hd_band_flux_wave_kernel, dim3(nblk(m, 4)), dim3(256), 0, s, flux,
+                       weight, nwave, m, bflux);
+  }
   return hd::launched("hd_band_flux");
 }
 

@@ -112,6 +112,7 @@ class Disort(RTSolver):
 
     def __init__(self, options: Optional[DisortOptions] = None):
         self.options = options if options is not None else DisortOptions()
+        self._waves = None
         self.reset()
 
     def reset(self):
@@ -189,8 +190,13 @@ class Disort(RTSolver):
             if tuple(tf.shape) != (ncol, nlyr + 1):
                 raise RuntimeError(f"Disort.forward: temf must be (ncol, nlyr+1) = "
                                    f"{(ncol, nlyr + 1)}, got {tuple(tf.shape)}")
-            wl = torch.tensor(op.wave_lower(), dtype=f64, device=dev)
-            wu = torch.tensor(op.wave_upper(), dtype=f64, device=dev)
+            # cached per device: no host->device copy per call (keeps forward
+            # capturable into a HIP graph once warmed up)
+            key = (str(dev), tuple(op.wave_lower()), tuple(op.wave_upper()))
+            if self._waves is None or self._waves[0] != key:
+                self._waves = (key, torch.tensor(op.wave_lower(), dtype=f64, device=dev),
+                               torch.tensor(op.wave_upper(), dtype=f64, device=dev))
+            wl, wu = self._waves[1], self._waves[2]
             keep += [tf, wl, wu]
         if out is None or out.device != dev:
             flux = torch.empty((nwave, ncol, nlyr + 1, 2), dtype=f64, device=dev)

@@ -79,6 +79,16 @@ def test_band_optics_matches_oracle(nprop):
     assert np.all(got[:, 2].cpu().numpy() == 0.0)  # empty column: tau 0, ssa 0 (not NaN)
 
 
+def test_band_flux_many_bins_few_outputs():
+    """one column line-by-line (C3-like): the wave-per-output reduction"""
+    from pyharp_amd.spectral import band_flux
+    rng = np.random.default_rng(61)
+    flux = rng.uniform(0, 1, (19990, 1, 11, 2))
+    w = rng.uniform(0, 0.1, 19990)
+    b = band_flux(torch.as_tensor(flux, device=DEV), torch.as_tensor(w, device=DEV))
+    np.testing.assert_allclose(b.cpu().numpy(), H.band_flux(flux, w), rtol=1e-12)
+
+
 def test_band_flux_heating_spherical_match_oracle():
     from pyharp_amd.spectral import band_flux, heating_rate, spherical_flux_correction
     rng = np.random.default_rng(6)
