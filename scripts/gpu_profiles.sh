@@ -15,6 +15,8 @@ for c in c5 c1 c3; do
   echo "[prof] $(date +%T) bench $c"
   timeout -k 10 300 python bench.py --config $c --steps 3 --warmup 1 > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err"
 done
+echo "[prof] $(date +%T) bench c1 graph"
+timeout -k 10 300 python bench.py --config c1 --graph --steps 50 --warmup 5 > "$OUT/bench_c1_graph.json" 2> "$OUT/bench_c1_graph.err"
 echo "[prof] $(date +%T) rocprof c4"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c4" -o kt --output-format csv -- \
     python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > "$OUT/prof_c4.json" 2> "$OUT/prof_c4.err"
