@@ -42,6 +42,7 @@ struct hd_context {
   hipEvent_t ev_back[2] = {nullptr, nullptr};
   hipEvent_t ev_pro[2] = {nullptr, nullptr};  // next chunk's prologue done (side stream)
   hipEvent_t ev_fork = nullptr;                // start of a solve on the caller's stream
+  double* sink = nullptr;                      // team kernels: stores of lanes >= nstr/2
 };
 
 namespace {
@@ -259,6 +260,7 @@ int hd_context_create(hd_context** out, int device) {
   HD_HIP(ctx, hipMalloc(&ctx->anyerr, sizeof(int)));
   HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
   HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+  HD_HIP(ctx, hipMalloc(&ctx->sink, 4096 * sizeof(double)));
   for (int b = 0; b < 2; ++b) {
     HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_sweep[b], hipEventDisableTiming));
     HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_back[b], hipEventDisableTiming));
@@ -280,6 +282,7 @@ int hd_context_destroy(hd_context* ctx) {
     if (ctx->ev_pro[b]) (void)hipEventDestroy(ctx->ev_pro[b]);
   }
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+  if (ctx->sink) (void)hipFree(ctx->sink);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   for (auto& e : ctx->pool)
     if (e) (void)hipEventDestroy(e);
@@ -448,6 +451,7 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
     la.nmom = nm;
     la.planck = planck;
     la.max_sweeps = 16;
+    la.sink = ctx->sink;
     hd::SweepArgs sa{};
     sa.scr = layer_ops;
     sa.bsub = bsub_b[buf];
@@ -465,6 +469,7 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
     sa.ncol = in->ncol;
     sa.nlyr = nlyr;
     sa.planck = planck;
+    sa.sink = ctx->sink;
     hipEvent_t* ev = nullptr;
     if (ctx->timing) {
       if (ctx->pool_used >= 3 * 512) {

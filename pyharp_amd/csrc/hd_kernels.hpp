@@ -67,6 +67,7 @@ struct LayerArgs {
   int nmom;   // moments used = min(nmom, nprop-2)
   int planck;
   int max_sweeps;
+  double* sink;  // team path: store target of lanes >= NN (>= 2*16^2+2*16+2 doubles)
 };
 
 struct SweepArgs {
@@ -86,6 +87,7 @@ struct SweepArgs {
   int ncol;
   int nlyr;
   int planck;
+  double* sink;  // team path: store target of lanes >= NN
 };
 
 struct QuadHost {

@@ -320,11 +320,14 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_layer_kernel(LayerArgs A) 
   const int np = A.nprop;
   int st = 0;
 
-  const double mu_i = act ? Qc.mu[ii] : 1.0;
-  const double sd_i = act ? Qc.sd[ii] : 0.0;
-  const double g_i = act ? Qc.g[ii] : 0.0;
-  const double rmu_i = act ? Qc.rmu[ii] : 0.0;
-  const double rg_i = act ? Qc.rg[ii] : 0.0;
+  // lanes >= NN carry zeros; masks are arithmetic (x * msk on clamped, finite
+  // loads) rather than selects around loads, which cost registers at NN < 16
+  const double msk = act ? 1.0 : 0.0;
+  const double mu_i = fma(msk, Qc.mu[ii] - 1.0, 1.0);
+  const double sd_i = Qc.sd[ii] * msk;
+  const double g_i = Qc.g[ii] * msk;
+  const double rmu_i = Qc.rmu[ii] * msk;
+  const double rg_i = Qc.rg[ii] * msk;
 
   // ---- inputs of this layer (harp layer L-1-lc) + delta-M (c_setdis) ----
   const double* q = A.prop + ((size_t)s * L + (L - 1 - lc)) * np;
@@ -362,8 +365,8 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_layer_kernel(LayerArgs A) 
       const double po0 = ((2 * lo - 1) * mub * pcur - (lo - 1) * pprev) / lo;
       pprev = po0;
       pcur = ((2 * lo + 1) * mub * po0 - lo * pe0) / (lo + 1);
-      const double ue = act ? ge * Qc.pt[le][ii] : 0.0;
-      const double uo = act ? go * Qc.pt[lo][ii] : 0.0;
+      const double ue = ge * Qc.pt[le][ii] * msk;
+      const double uo = go * Qc.pt[lo][ii] * msk;
       xs = fma(ue, pe0, xs);
       xd = fma(uo, po0, xd);
       sfor<0, NN>([&](auto J) {
@@ -411,7 +414,7 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_layer_kernel(LayerArgs A) 
     cvec = sd_i * mu_i;
     team_lsolve<NN>(lch, rdl, cvec);
     team_usolve<NN>(lt, rdl, cvec);
-    cvec = act ? fma(b1 * rg_i, cvec, db) : 0.0;
+    cvec = fma(b1 * rg_i, cvec, db) * msk;
   }
 
   // ---- eigenpairs (c_soleig): Sym = L^T (-A+) L = V diag(k^2) V^T ----
@@ -433,7 +436,7 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_layer_kernel(LayerArgs A) 
     double k2 = 0.0;
     sfor<0, NN>([&](auto K) { k2 = fma(bcol[HD_K(K)], bcol[HD_K(K)], k2); });
     if (act && !(k2 > 0.0)) st |= kStEigen;
-    kk = act ? sqrt(k2 > 0.0 ? k2 : 0.0) : 0.0;
+    kk = sqrt(k2 > 0.0 ? k2 : 0.0) * msk;
     // v_j = B0^-1 b_j = L^-1 C^-T b_j (lane-local solves, matrix entries broadcast)
     sfor_rev<0, NN>([&](auto I) {  // C^T y = b
       constexpr int r = HD_K(I);
@@ -445,7 +448,7 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_layer_kernel(LayerArgs A) 
       constexpr int r = HD_K(I);
       double t = bcol[r];
       sfor<0, r>([&](auto K) { t = fma(-bc<r>(lch[HD_K(K)]), vt[HD_K(K)], t); });
-      vt[r] = act ? t * bc<r>(rdl) : 0.0;
+      vt[r] = t * bc<r>(rdl) * msk;
     });
   }
   // v = rows of V (lane i: V_ij over j): transpose through this team's LDS
@@ -456,7 +459,7 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_layer_kernel(LayerArgs A) 
     double* tile = tr_lds + (threadIdx.x >> 4) * (kTeam * (kTeam + 1));
     sfor<0, NN>([&](auto I) { tile[HD_K(I) * (kTeam + 1) + i] = vt[HD_K(I)]; });
     __builtin_amdgcn_wave_barrier();
-    sfor<0, NN>([&](auto J) { v[HD_K(J)] = act ? tile[i * (kTeam + 1) + HD_K(J)] : 0.0; });
+    sfor<0, NN>([&](auto J) { v[HD_K(J)] = tile[ii * (kTeam + 1) + HD_K(J)] * msk; });
     __builtin_amdgcn_wave_barrier();
   }
 
@@ -471,7 +474,7 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_layer_kernel(LayerArgs A) 
       st |= kStResonance;
       den = den < 0.0 ? -1.0e-9 * r2 : 1.0e-9 * r2;
     }
-    const double tt = act ? t / den : 0.0;
+    const double tt = t / den * msk;
     double y = 0.0;  // V tt
     sfor<0, NN>([&](auto J) { y = fma(v[HD_K(J)], bc<HD_K(J)>(tt), y); });
     double sv = 0.0;  // W^-1 D^1/2 L y
@@ -586,25 +589,26 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_layer_kernel(LayerArgs A) 
   }
 
   // ---- store: R~ = Q~- + Q~+, T~ = I - Q~- + Q~+ (rows), S~+, S~-, tau' ----
-  double* out = A.scr + ((size_t)lc * A.nsc + sl) * ne1t<NN>();
+  // lanes >= NN store into a sink instead of branching around the stores (a
+  // branch here costs the whole kernel's register allocation at NN < 16)
+  double* rec = A.scr + ((size_t)lc * A.nsc + sl) * ne1t<NN>();
+  double* out = act ? rec : A.sink;
   double chk = 0.0;
-  if (act) {
-    sfor<0, NN>([&](auto J) {
-      constexpr int j = HD_K(J);
-      const double r = qm[j] + qp[j];
-      const double t = (i == j ? 1.0 : 0.0) - qm[j] + qp[j];
-      out[i * NN + j] = r;
-      out[NN * NN + i * NN + j] = t;
-      chk += r + t;
-    });
-    const double sp = g_i * (zp * (1.0 - e0) - db) + pv - qv;
-    const double sm = g_i * (-zm * (1.0 - e0) + db) - pv - qv;
-    out[2 * NN * NN + i] = sp;
-    out[2 * NN * NN + NN + i] = sm;
-    chk += sp + sm;
-  }
-  if (i == 0) out[2 * NN * NN + 2 * NN] = taup;
-  if (!isfinite(chk + taup)) st |= kStNonFinite;
+  sfor<0, NN>([&](auto J) {
+    constexpr int j = HD_K(J);
+    const double r = qm[j] + qp[j];
+    const double t = (i == j ? 1.0 : 0.0) - qm[j] + qp[j];
+    out[ii * NN + j] = r;
+    out[NN * NN + ii * NN + j] = t;
+    chk += r + t;
+  });
+  const double sp = g_i * (zp * (1.0 - e0) - db) + pv - qv;
+  const double sm = g_i * (-zm * (1.0 - e0) + db) - pv - qv;
+  out[2 * NN * NN + ii] = sp;
+  out[2 * NN * NN + NN + ii] = sm;
+  chk += sp + sm;
+  if (i == 0) rec[2 * NN * NN + 2 * NN] = taup;
+  if (act && !isfinite(chk + taup)) st |= kStNonFinite;
   if (st) {
     atomicOr(&A.status[s], st);
     if (st & 0x0F) atomicOr(A.anyerr, 1);
@@ -627,7 +631,8 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_sweep_kernel(SweepArgs A) 
   const int L = A.nlyr;
   const size_t nsc = A.nsc;
   int st = 0;
-  const double g_i = act ? Qc.g[ii] : 0.0;
+  const double msk = act ? 1.0 : 0.0;  // arithmetic lane mask (see the layer kernel)
+  const double g_i = Qc.g[ii] * msk;
 
   const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
   const double fb = A.fbeam ? A.fbeam[s] : 0.0;
@@ -652,16 +657,17 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_sweep_kernel(SweepArgs A) 
   for (int lc = 0; lc < L; ++lc) {
     const double* rec = A.scr + ((size_t)lc * nsc + sl) * ne1t<NN>();
     double* bp = A.bsub + ((size_t)lc * nsc + sl) * ne2t<NN>();
+    double* bw = act ? bp : A.sink;  // lanes >= NN store into the sink (no branches)
     double rl[NN];
-    sfor<0, NN>([&](auto J) { rl[HD_K(J)] = act ? rec[ii * NN + HD_K(J)] : 0.0; });
-    const double spl = act ? rec[2 * NN * NN + ii] : 0.0;
-    const double sml = act ? rec[2 * NN * NN + NN + ii] : 0.0;
+    sfor<0, NN>([&](auto J) { rl[HD_K(J)] = rec[ii * NN + HD_K(J)] * msk; });
+    const double spl = rec[2 * NN * NN + ii] * msk;
+    const double sml = rec[2 * NN * NN + NN + ii] * msk;
 
     // level lc (top of layer lc): F_dn = rc . I+ + cs
     {
       double t = 0.0;
       sfor<0, NN>([&](auto J) { t = fma(ra[HD_K(J)], Qc.g[HD_K(J)], t); });
-      if (act) bp[NN * NN + NN + i] = twopi * t;
+      bw[NN * NN + NN + ii] = twopi * t;
       const double cs = team_sum(g_i * sd);
       if (i == 0) bp[NN * NN + 2 * NN] = fma(twopi, cs, f0mu0 * exp(-tauc * rmu0));
     }
@@ -704,7 +710,7 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_sweep_kernel(SweepArgs A) 
     // u = A t1 + Sd
     double u = sd;
     sfor<0, NN>([&](auto K) { u = fma(ra[HD_K(K)], bc<HD_K(K)>(t1), u); });
-    if (act) bp[NN * NN + i] = t1;
+    bw[NN * NN + ii] = t1;
     // M1 = A W1^-1 (row-local): z U = a, then x L = z
     double am[NN];
     sfor<0, NN>([&](auto J) {
@@ -723,7 +729,7 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_sweep_kernel(SweepArgs A) 
     double tr[NN], zt[NN];
     sfor<0, NN>([&](auto J) {
       constexpr int j = HD_K(J);
-      tr[j] = act ? rec[NN * NN + ii * NN + j] : 0.0;
+      tr[j] = rec[NN * NN + ii * NN + j] * msk;
       zt[j] = tr[j];
     });
     sfor<0, NN>([&](auto K) {
@@ -738,7 +744,7 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_sweep_kernel(SweepArgs A) 
       const double m = i < k ? w[k] : 0.0;
       sfor<0, NN>([&](auto J) { zt[HD_K(J)] = fma(-m, bc<k>(zt[HD_K(J)]), zt[HD_K(J)]); });
     });
-    if (act) sfor<0, NN>([&](auto J) { bp[i * NN + HD_K(J)] = zt[HD_K(J)]; });
+    sfor<0, NN>([&](auto J) { bw[ii * NN + HD_K(J)] = zt[HD_K(J)]; });
     // P = M1 T ; Ra <- R_l + T P ; Sd <- T u + S-
     double pm[NN];
     sfor<0, NN>([&](auto J) {
@@ -785,12 +791,12 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_sweep_kernel(SweepArgs A) 
   // ---- back-substitution bottom -> top ----
   for (int lc = L - 1; lc >= 0; --lc) {
     const double* bp = A.bsub + ((size_t)lc * nsc + sl) * ne2t<NN>();
-    double nip = act ? bp[NN * NN + ii] : 0.0;
+    double nip = bp[NN * NN + ii] * msk;
     sfor<0, NN>([&](auto J) {
-      const double z = act ? bp[ii * NN + HD_K(J)] : 0.0;
+      const double z = bp[ii * NN + HD_K(J)] * msk;
       nip = fma(z, bc<HD_K(J)>(ip), nip);
     });
-    const double rc = act ? bp[NN * NN + NN + ii] : 0.0;
+    const double rc = bp[NN * NN + NN + ii] * msk;
     const double up = team_sum(g_i * nip);
     const double dn = team_sum(rc * nip);
     ip = nip;
