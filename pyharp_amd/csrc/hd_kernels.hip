@@ -239,7 +239,9 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
   double db = 0.0, bsum = 0.0;
   if (A.planck) {
     const double bt = A.planckv[(size_t)(L - lc) * A.nsc + sl];
-    const double bb = A.planckv[(size_t)(L - lc - 1) * A.nsc + sl];
+    // a transparent layer carries its top level's Planck value through
+    // (c_disort's xr1 = 0 when dtaucpr = 0: B(tau) = xr0 = B_top)
+    const double bb = taup > 0.0 ? A.planckv[(size_t)(L - lc - 1) * A.nsc + sl] : bt;
     db = bb - bt;
     bsum = bt + bb;
     const double b1 = taup > 0.0 ? 2.0 * db / taup : 0.0;

@@ -198,10 +198,19 @@ class Disort(RTSolver):
                                torch.tensor(op.wave_upper(), dtype=f64, device=dev))
             wl, wu = self._waves[1], self._waves[2]
             keep += [tf, wl, wu]
-        if out is None or out.device != dev:
+        if out is None:
             flux = torch.empty((nwave, ncol, nlyr + 1, 2), dtype=f64, device=dev)
         else:
+            if (out.device != dev or out.dtype != f64 or not out.is_contiguous()
+                    or tuple(out.shape) != (nwave, ncol, nlyr + 1, 2)):
+                raise RuntimeError("Disort.forward: out must be a contiguous float64 tensor "
+                                   f"of shape {(nwave, ncol, nlyr + 1, 2)} on {dev}")
             flux = out
+        if status is not None and (status.device != dev or status.dtype != torch.int32
+                                   or not status.is_contiguous()
+                                   or status.numel() < nwave * ncol):
+            raise RuntimeError(f"Disort.forward: status must be a contiguous int32 tensor of "
+                               f">= {nwave * ncol} elements on {dev}")
 
         def ptr(t):
             return t.data_ptr() if t is not None else None

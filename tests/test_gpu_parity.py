@@ -369,3 +369,43 @@ def test_graph_capture_replay(nstr):
     ref2 = d.forward(p, b)
     assert torch.equal(out, ref2)
     assert not torch.equal(ref2, ref)
+
+
+def test_out_and_status_buffers_are_validated():
+    d = _disort(8, 3, 1, 2)
+    dev = torch.device("cuda", 0)
+    prop = torch.zeros((1, 2, 3, 10), dtype=torch.float64, device=dev)
+    with pytest.raises(RuntimeError, match="out must be"):
+        d.forward(prop, {}, out=torch.empty((1, 2, 3, 2), dtype=torch.float64, device=dev))
+    with pytest.raises(RuntimeError, match="status must be"):
+        d.forward(prop, {}, status=torch.zeros(1, dtype=torch.int32, device=dev))
+
+
+@pytest.mark.parametrize("nstr", [4, 8, 16, 24, 32])
+def test_planck_edge_cases(oracle_c, nstr):
+    """Both paths (register nstr <= 16, team 18..32) on the edge cases with
+    Planck on and every boundary key (fisot, temis/ttemp, btemp).  Column 0 is
+    transparent over a temperature gradient: a zero-depth layer carries its top
+    level's Planck value (xr1 = 0), so both fluxes stay constant."""
+    nlyr = 6
+    prop = np.zeros((1, 6, nlyr, 2 + nstr))
+    prop[..., 0] = 0.5
+    prop[0, 0, :, 0] = 0.0          # fully transparent column
+    prop[0, 1, :, 1] = 1.0          # conservative
+    prop[0, 2, 2, 0] = 0.0          # one empty layer
+    prop[0, 3, :, 1] = 0.5          # isotropic (no moments)
+    prop[0, 4, :, 0] = 50.0         # optically very thick
+    prop[0, 5, :, 1] = 0.95
+    for l in range(nstr):
+        prop[0, 5, :, 2 + l] = 0.85 ** (l + 1)
+    bc = {"fbeam": np.ones((1, 6)), "umu0": np.array([[1.0, 0.5, 0.3, 0.9, 0.7, 0.2]]),
+          "albedo": np.array([[0.0, 1.0, 0.5, 0.2, 0.3, 0.0]]),
+          "fisot": np.full((1, 6), 0.01), "temis": np.full((1, 6), 0.5),
+          "ttemp": np.full((1, 6), 200.0), "btemp": np.full((1, 6), 280.0)}
+    from oracle.disort_np import layer2level
+    temf = layer2level(np.linspace(280.0, 200.0, nlyr)[None, :].repeat(6, 0))
+    wl, wu = np.array([500.0]), np.array([800.0])
+    ref = oracle_c.forward(prop, bc, temf, nstr=nstr, planck=True, wave_lower=wl, wave_upper=wu)
+    d = _disort(nstr, nlyr, 1, 6, planck=True, wl=wl, wu=wu)
+    f = _run(d, prop, bc, temf)
+    assert rel_err(f, ref).max() < TOL
