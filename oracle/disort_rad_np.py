@@ -1,0 +1,389 @@
+"""Numpy FP64 restatement of DISORT's intensity path (all azimuthal modes,
+user optical depths ``usrtau``, user polar/azimuth angles ``usrang``).
+
+TEST INFRASTRUCTURE ONLY.  Nothing in ``pyharp_amd`` imports this module; only
+``tests/`` and ``__graft_entry__.smoke()`` may use it, and only as the checker.
+
+What this follows
+-----------------
+The reference's intensity call site is ``tests/test_disort.cpp:13-55``
+(flags ``usrtau,usrang``; ``user_mu``, ``user_phi``, ``user_tau``;
+``disort->get_rad()``) and the legacy driver
+``src/rtsolver/rt_solver_disort.cpp_:210-286`` (``c_disort`` then
+``ds_out_.uu`` interpolated onto outgoing rays).  The arithmetic is cdisort
+2.1.3 inside pydisort @ ``afee3ec897f`` (absent here),
+so this module restates the published DISORT method (Stamnes, Tsay,
+Wiscombe & Jayaweera 1988; DISORT 2.0 report) with cdisort's stage
+structure, re-using the flux oracle's stages (``oracle/disort_np.py``):
+
+==============  ===========================================================
+cdisort stage   here
+==============  ===========================================================
+c_lepoly        :func:`lepoly` (normalised associated Legendre Y_l^m)
+c_setdis        ``disort_np.setdis`` + :func:`_user_taus` (utau -> utaupr)
+c_soleig        ``disort_np.soleig`` on the mode-m CC matrix
+c_upbeam        :func:`_upbeam_m` (factor 2 - delta_m0 on the beam source)
+c_upisot        ``disort_np.upisot`` (m = 0 only)
+c_setmtx/solve0 :func:`_solve_mode` (Lambertian: surface terms only at m=0)
+c_usrint        :func:`_user_intensity` (source-function integration along
+                the ray, closed-form exponential integrals)
+c_fluxes        :func:`disort_rad_column` (fluxes at the user depths)
+azimuth sum     uu = sum_m uum cos(m (phi - phi0)), phi in degrees
+==============  ===========================================================
+
+Not restated: the Nakajima-Tanaka intensity corrections (``intensity_correction``,
+``old_intensity_correction``).  They vanish when the delta-M truncation does
+(f = chi_nstr = 0, e.g. isotropic or Rayleigh phase functions, the
+``tests/test_disort.cpp`` configuration); the parity tests use such phase
+functions wherever intensities are compared.
+
+Parity status: **parity unpinned** against cdisort (absent).  Pinned by known
+answers in ``tests/test_rad_oracle.py``: quadrature-angle intensities equal the
+banded solution's, fluxes at the levels equal ``disort_np``'s, the omega=0
+slab's beam-reflection and thermal radiances in closed form / by independent
+quadrature, and the single-scattering radiance of an optically thin Rayleigh
+layer including its azimuth dependence.
+"""
+
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import scipy.linalg
+
+from .disort_np import double_gauss, plkavg, setdis, soleig, upisot
+
+
+def lepoly(nstr: int, m: int, mu) -> np.ndarray:
+    """Y_l^m(mu) = sqrt((l-m)!/(l+m)!) P_l^m(mu) for l = 0..nstr-1 (0 for l < m).
+
+    Shape (nstr, len(mu)).  The Condon-Shortley sign is irrelevant here: every
+    use is a product Y_l^m(a) Y_l^m(b).
+    """
+    mu = np.atleast_1d(np.asarray(mu, np.float64))
+    y = np.zeros((nstr, mu.size))
+    if m >= nstr:
+        return y
+    c = 1.0
+    for i in range(1, m + 1):
+        c *= math.sqrt((2 * i - 1) / (2 * i))
+    y[m] = c * np.sqrt(np.maximum(0.0, 1.0 - mu * mu)) ** m
+    if m + 1 < nstr:
+        y[m + 1] = math.sqrt(2 * m + 1) * mu * y[m]
+    for l in range(m + 2, nstr):
+        y[l] = ((2 * l - 1) * mu * y[l - 1] - math.sqrt((l - 1) ** 2 - m * m) * y[l - 2]) \
+            / math.sqrt(l * l - m * m)
+    return y
+
+
+def _upbeam_m(cc, cmu_full, gl_lc, ylm, ylm0, umu0, fbeam, m):
+    fac = (2.0 - (m == 0)) * fbeam / (4.0 * math.pi)
+    x0 = fac * (ylm.T @ (gl_lc * ylm0))
+    a = np.diag(1.0 + cmu_full / umu0) - cc
+    return np.linalg.solve(a, x0)
+
+
+def _user_taus(utau, dtauc, dtaucp, tauc, taucpr):
+    """(layer index, scaled depth) of every user optical depth (c_setdis)."""
+    nlyr = dtauc.size
+    lay = np.zeros(len(utau), int)
+    upr = np.zeros(len(utau))
+    for k, u in enumerate(utau):
+        if u < -1e-12 or u > tauc[-1] * (1 + 1e-12) + 1e-300:
+            raise ValueError("user_tau outside [0, total optical depth]")
+        lc = int(np.searchsorted(tauc[1:], u, side="left"))
+        lc = min(lc, nlyr - 1)
+        lay[k] = lc
+        frac = dtaucp[lc] / dtauc[lc] if dtauc[lc] > 0 else 0.0
+        upr[k] = taucpr[lc] + frac * (u - tauc[lc])
+    return lay, upr
+
+
+def _phi(x):
+    """(1 - exp(-x)) / x, = 1 at x = 0."""
+    return 1.0 if x == 0.0 else -math.expm1(-x) / x
+
+
+def _seg_exp(a, c, tref, t1, t2, tau, mu):
+    """int_{t1}^{t2} a exp(-c (t - tref)) exp(-(t - tau)/mu) dt/mu (t1 nearer tau)."""
+    p1 = math.exp(-c * (t1 - tref) - (t1 - tau) / mu)
+    den = 1.0 + c * mu
+    x = den * (t2 - t1) / mu
+    if abs(x) < 0.5:
+        return a * p1 * (t2 - t1) / mu * _phi(x)
+    p2 = math.exp(-c * (t2 - tref) - (t2 - tau) / mu)
+    return a * (p1 - p2) / den
+
+
+def _seg_lin(a0, a1, t1, t2, tau, mu):
+    """int_{t1}^{t2} (a0 + a1 t) exp(-(t - tau)/mu) dt/mu."""
+    e1 = math.exp(-(t1 - tau) / mu)
+    e2 = math.exp(-(t2 - tau) / mu)
+    return (a0 + a1 * t1 + a1 * mu) * e1 - (a0 + a1 * t2 + a1 * mu) * e2
+
+
+def disort_rad_column(dtauc, ssalb, pmom, nstr, *, umu, phi, utau, umu0=1.0, phi0=0.0,
+                      fbeam=0.0, albedo=0.0, fisot=0.0, planck=False, temper=None,
+                      btemp=0.0, ttemp=0.0, temis=0.0, wvnmlo=0.0, wvnmhi=0.0,
+                      onlyfl=False):
+    """One DISORT solve with intensities (layers top->bottom, cdisort order).
+
+    umu: user polar cosines (nonzero), phi: user azimuths [deg], utau: user
+    optical depths (unscaled, ascending).  Returns dict with ``uu``
+    (nphi, ntau, numu) and ``flup``, ``rfldir``, ``rfldn``, ``fdn`` at utau.
+    """
+    dtauc = np.atleast_1d(np.asarray(dtauc, np.float64))
+    nlyr = dtauc.size
+    if nstr < 2 or nstr % 2:
+        raise ValueError("nstr must be even and >= 2")
+    nn = nstr // 2
+    pmom = np.asarray(pmom, np.float64).reshape(nlyr, -1)
+    umu = np.atleast_1d(np.asarray(umu, np.float64))
+    phi = np.atleast_1d(np.asarray(phi, np.float64))
+    utau = np.atleast_1d(np.asarray(utau, np.float64))
+    cmu, cwt = double_gauss(nn)
+    cmu_full = np.concatenate([cmu, -cmu])
+    cwt_full = np.concatenate([cwt, cwt])
+    dtaucp, taucpr, tauc, oprim, gl = setdis(dtauc, ssalb, pmom, nstr)
+    lay, utaupr = _user_taus(utau, dtauc, dtaucp, tauc, taucpr)
+    beam = fbeam > 0.0 and umu0 > 0.0
+    if planck:
+        pkag = np.array([plkavg(wvnmlo, wvnmhi, t) for t in temper])
+        bplanck = plkavg(wvnmlo, wvnmhi, btemp)
+        tplanck = plkavg(wvnmlo, wvnmhi, ttemp) * temis
+    else:
+        pkag = np.zeros(nlyr + 1)
+        bplanck = tplanck = 0.0
+    nmode = nstr if (beam and not onlyfl) else 1
+    ntau, numu = utau.size, umu.size
+    uum = np.zeros((nmode, ntau, numu))
+    out = {}
+    for m in range(nmode):
+        sol = _solve_mode(m, nstr, nn, nlyr, cmu, cwt, cmu_full, cwt_full, dtaucp, taucpr,
+                          oprim, gl, beam, umu0, fbeam, albedo, fisot, planck, pkag,
+                          bplanck, tplanck)
+        if m == 0:
+            out.update(_fluxes_at(sol, lay, utaupr, utau, nn, cmu, cwt, beam, umu0, fbeam))
+        if not onlyfl:
+            uum[m] = _user_intensity(sol, m, nstr, nn, nlyr, umu, lay, utaupr, cmu, cwt,
+                                     cmu_full, cwt_full, taucpr, oprim, gl, beam, umu0,
+                                     fbeam, albedo, fisot, planck, bplanck, tplanck)
+    cosm = np.cos(np.outer(np.arange(nmode), np.radians(phi - phi0)))  # (nmode, nphi)
+    out["uu"] = np.einsum("mj,mtu->jtu", cosm, uum)
+    out["uum"] = uum
+    return out
+
+
+def _solve_mode(m, nstr, nn, nlyr, cmu, cwt, cmu_full, cwt_full, dtaucp, taucpr, oprim, gl,
+                beam, umu0, fbeam, albedo, fisot, planck, pkag, bplanck, tplanck):
+    """Mode-m homogeneous/particular solutions and the boundary-value constants."""
+    ylm = lepoly(nstr, m, cmu_full)
+    ylm0 = lepoly(nstr, m, [-umu0])[:, 0] if beam else np.zeros(nstr)
+    therm = planck and m == 0
+    kk = np.zeros((nlyr, nn))
+    gc = np.zeros((nlyr, nstr, nstr))
+    zb = np.zeros((nlyr, nstr))
+    z0 = np.zeros((nlyr, nstr))
+    z1 = np.zeros((nlyr, nstr))
+    xr = np.zeros((nlyr, 2))
+    for lc in range(nlyr):
+        cc = 0.5 * (ylm.T * gl[lc]) @ ylm * cwt_full[None, :]
+        k, gp, gm = soleig(cc, cmu)
+        kk[lc] = k
+        gc[lc, :nn, :nn] = gp
+        gc[lc, nn:, :nn] = gm
+        gc[lc, :nn, nn:] = gm
+        gc[lc, nn:, nn:] = gp
+        if beam:
+            zb[lc] = _upbeam_m(cc, cmu_full, gl[lc], ylm, ylm0, umu0, fbeam, m)
+        if therm:
+            xr1 = (pkag[lc + 1] - pkag[lc]) / dtaucp[lc] if dtaucp[lc] > 0 else 0.0
+            xr0 = pkag[lc] - xr1 * taucpr[lc]
+            xr[lc] = (xr0, xr1)
+            z0[lc], z1[lc] = upisot(cc, cmu_full, oprim[lc], xr0, xr1)
+
+    def zpart(lc, tau):
+        v = z0[lc] + z1[lc] * tau
+        if beam:
+            v = v + zb[lc] * math.exp(-tau / umu0)
+        return v
+
+    ee = np.exp(-kk * dtaucp[:, None])
+
+    def top_cols(lc):
+        return gc[lc] * np.concatenate([np.ones(nn), ee[lc]])[None, :]
+
+    def bot_cols(lc):
+        return gc[lc] * np.concatenate([ee[lc], np.ones(nn)])[None, :]
+
+    ncol = nstr * nlyr
+    a = np.zeros((ncol, ncol))
+    b = np.zeros(ncol)
+    a[:nn, :nstr] = top_cols(0)[nn:, :]
+    b[:nn] = (fisot + tplanck if m == 0 else 0.0) - zpart(0, 0.0)[nn:]
+    for lc in range(nlyr - 1):
+        r0 = nn + lc * nstr
+        a[r0:r0 + nstr, lc * nstr:(lc + 1) * nstr] = bot_cols(lc)
+        a[r0:r0 + nstr, (lc + 1) * nstr:(lc + 2) * nstr] = -top_cols(lc + 1)
+        tau = taucpr[lc + 1]
+        b[r0:r0 + nstr] = zpart(lc + 1, tau) - zpart(lc, tau)
+    r0 = nn + (nlyr - 1) * nstr
+    lb = bot_cols(nlyr - 1)
+    alb = albedo if m == 0 else 0.0
+    refl = 2.0 * alb * (cwt * cmu)
+    a[r0:r0 + nn, (nlyr - 1) * nstr:] = lb[:nn, :] - refl[None, :] @ lb[nn:, :]
+    zbt = zpart(nlyr - 1, taucpr[nlyr])
+    rhs = np.full(nn, (1.0 - alb) * bplanck if m == 0 else 0.0)
+    if beam and m == 0:
+        rhs += alb * umu0 * fbeam * math.exp(-taucpr[nlyr] / umu0) / math.pi
+    b[r0:r0 + nn] = rhs - (zbt[:nn] - refl @ zbt[nn:])
+    bw = 3 * nn - 1
+    ab = np.zeros((2 * bw + 1, ncol))
+    for j in range(ncol):
+        lo = max(0, j - bw)
+        hi = min(ncol, j + bw + 1)
+        ab[bw + lo - j:bw + hi - j, j] = a[lo:hi, j]
+    ll = scipy.linalg.solve_banded((bw, bw), ab, b).reshape(nlyr, nstr)
+
+    def quad_field(lc, tau):
+        """quadrature intensities (+mu_i then -mu_i) at scaled depth tau in layer lc"""
+        e = np.concatenate([np.exp(-kk[lc] * (tau - taucpr[lc])),
+                            np.exp(-kk[lc] * (taucpr[lc + 1] - tau))])
+        return gc[lc] @ (ll[lc] * e) + zpart(lc, tau)
+
+    return dict(kk=kk, gc=gc, zb=zb, z0=z0, z1=z1, xr=xr, ll=ll, quad_field=quad_field)
+
+
+def _fluxes_at(sol, lay, utaupr, utau, nn, cmu, cwt, beam, umu0, fbeam):
+    wmu = cwt * cmu
+    ntau = utau.size
+    flup = np.zeros(ntau)
+    dfdn = np.zeros(ntau)
+    for k in range(ntau):
+        u = sol["quad_field"](lay[k], utaupr[k])
+        flup[k] = 2.0 * math.pi * u[:nn] @ wmu
+        dfdn[k] = 2.0 * math.pi * u[nn:] @ wmu
+    if beam:
+        rfldir = umu0 * fbeam * np.exp(-utau / umu0)
+        fdn = dfdn + umu0 * fbeam * np.exp(-utaupr / umu0)
+    else:
+        rfldir = np.zeros(ntau)
+        fdn = dfdn
+    return {"flup": flup, "rfldir": rfldir, "rfldn": fdn - rfldir, "fdn": fdn}
+
+
+def _user_intensity(sol, m, nstr, nn, nlyr, umu, lay, utaupr, cmu, cwt, cmu_full, cwt_full,
+                    taucpr, oprim, gl, beam, umu0, fbeam, albedo, fisot, planck, bplanck,
+                    tplanck):
+    """Mode-m radiance at every (user depth, user angle) by integrating the
+    source function along the ray through the layers (c_usrint)."""
+    kk, gc, zb, z0, z1, xr, ll = (sol[k] for k in ("kk", "gc", "zb", "z0", "z1", "xr", "ll"))
+    ylm = lepoly(nstr, m, cmu_full)
+    ylmu = lepoly(nstr, m, umu)
+    ylm0 = lepoly(nstr, m, [-umu0])[:, 0] if beam else np.zeros(nstr)
+    fac = (2.0 - (m == 0)) * fbeam / (4.0 * math.pi)
+    therm = planck and m == 0
+    ntau, numu = len(utaupr), umu.size
+    res = np.zeros((ntau, numu))
+    # per-layer source coefficients at every user angle
+    hmode = np.zeros((nlyr, numu, nstr))   # scattering of each homogeneous mode
+    sbeam = np.zeros((nlyr, numu))         # amplitude of exp(-t/umu0), absolute t
+    sth0 = np.zeros((nlyr, numu))          # a0 + a1 t (absolute t)
+    sth1 = np.zeros((nlyr, numu))
+    for lc in range(nlyr):
+        cu = 0.5 * (ylmu.T * gl[lc]) @ ylm * cwt_full[None, :]     # (numu, 2nn), includes w
+        hmode[lc] = cu @ gc[lc]
+        if beam:
+            sbeam[lc] = fac * (ylmu.T @ (gl[lc] * ylm0)) + cu @ zb[lc]
+        if therm:
+            sth0[lc] = (1.0 - oprim[lc]) * xr[lc, 0] + cu @ z0[lc]
+            sth1[lc] = (1.0 - oprim[lc]) * xr[lc, 1] + cu @ z1[lc]
+    tb = taucpr[nlyr]
+    u_bot = sol["quad_field"](nlyr - 1, tb)
+    fdn_bot = 2.0 * math.pi * u_bot[nn:] @ (cwt * cmu)
+    if m == 0:
+        dirb = umu0 * fbeam * math.exp(-tb / umu0) if beam else 0.0
+        i_bot = albedo / math.pi * (fdn_bot + dirb) + (1.0 - albedo) * bplanck
+        i_top = fisot + tplanck
+    else:
+        i_bot = i_top = 0.0
+
+    def layer_integral(lc, iu, t1, t2, tau, mu):
+        s = 0.0
+        t0, tl = taucpr[lc], taucpr[lc + 1]
+        for j in range(nn):
+            s += _seg_exp(ll[lc, j] * hmode[lc, iu, j], kk[lc, j], t0, t1, t2, tau, mu)
+            s += _seg_exp(ll[lc, nn + j] * hmode[lc, iu, nn + j], -kk[lc, j], tl, t1, t2, tau,
+                          mu)
+        if beam:
+            s += _seg_exp(sbeam[lc, iu], 1.0 / umu0, 0.0, t1, t2, tau, mu)
+        if therm:
+            s += _seg_lin(sth0[lc, iu], sth1[lc, iu], t1, t2, tau, mu)
+        return s
+
+    for k in range(ntau):
+        tau, lu = utaupr[k], lay[k]
+        for iu, mu in enumerate(umu):
+            if mu > 0.0:
+                v = i_bot * math.exp(-(tb - tau) / mu)
+                for lc in range(lu, nlyr):
+                    v += layer_integral(lc, iu, max(tau, taucpr[lc]), taucpr[lc + 1], tau, mu)
+            else:
+                v = i_top * math.exp(tau / mu)
+                for lc in range(lu, -1, -1):
+                    v += layer_integral(lc, iu, min(tau, taucpr[lc + 1]), taucpr[lc], tau, mu)
+            res[k, iu] = v
+    return res
+
+
+def disort_rad_forward(prop, bc, temf=None, *, nstr, umu, phi, utau=None, nmom=None,
+                       planck=False, wave_lower=None, wave_upper=None, onlyfl=False):
+    """Batch driver with harp's layout (prop (W, C, L, nprop), layer 0 = bottom).
+
+    utau None = the nlyr+1 layer boundaries (top->bottom).  Returns
+    (flux (W, C, ntau, 2) with index 0 = the deepest user depth, [...,0] up,
+    [...,1] rfldir + rfldn;  uu (W, C, nphi, ntau, numu) in user order).
+    """
+    prop = np.asarray(prop, np.float64)
+    nwave, ncol, nlyr, nprop = prop.shape
+    nmom = nstr if nmom is None else nmom
+    nm = max(0, min(nmom, nprop - 2))
+
+    def bcv(key, default):
+        if key in bc and bc[key] is not None:
+            return np.broadcast_to(np.asarray(bc[key], np.float64), (nwave, ncol))
+        return np.full((nwave, ncol), default)
+
+    keys = dict(fbeam=0.0, umu0=1.0, phi0=0.0, albedo=0.0, btemp=0.0, ttemp=0.0, temis=0.0,
+                fisot=0.0)
+    v = {k: bcv(k, d) for k, d in keys.items()}
+    umu = np.atleast_1d(np.asarray(umu, np.float64))
+    phi = np.atleast_1d(np.asarray(phi, np.float64))
+    flux = uu = None
+    for w in range(nwave):
+        for c in range(ncol):
+            p = prop[w, c, ::-1]
+            pm = np.zeros((nlyr, nm + 1))
+            pm[:, 0] = 1.0
+            if nm:
+                pm[:, 1:] = p[:, 2:2 + nm]
+            ssa = p[:, 1] if nprop > 1 else np.zeros(nlyr)
+            ut = np.concatenate([[0.0], np.cumsum(p[:, 0])]) if utau is None else utau
+            kw = {}
+            if planck:
+                kw = dict(planck=True, temper=np.asarray(temf)[c, ::-1], btemp=v["btemp"][w, c],
+                          ttemp=v["ttemp"][w, c], temis=v["temis"][w, c],
+                          wvnmlo=wave_lower[w], wvnmhi=wave_upper[w])
+            r = disort_rad_column(p[:, 0], ssa, pm, nstr, umu=umu, phi=phi, utau=ut,
+                                  umu0=v["umu0"][w, c], phi0=v["phi0"][w, c],
+                                  fbeam=v["fbeam"][w, c], albedo=v["albedo"][w, c],
+                                  fisot=v["fisot"][w, c], onlyfl=onlyfl, **kw)
+            if flux is None:
+                ntau = len(ut)
+                flux = np.zeros((nwave, ncol, ntau, 2))
+                uu = np.zeros((nwave, ncol, phi.size, ntau, umu.size))
+            flux[w, c, :, 0] = r["flup"][::-1]
+            flux[w, c, :, 1] = r["fdn"][::-1]
+            uu[w, c] = r["uu"]
+    return flux, uu
