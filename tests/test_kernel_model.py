@@ -45,3 +45,46 @@ def test_model_exact_conservative_without_dither():
     finally:
         kernel_model.DITHER = saved
     assert np.all(np.isfinite(fu)) and np.abs(fd - fu).max() < 1e-12
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_radiance_model_matches_oracle(seed):
+    """tests/kernel_model_rad.py (the radiance kernels' formulation) vs the
+    radiance oracle, every azimuthal mode, user depths inside layers."""
+    import kernel_model_rad as km
+    from oracle.disort_np import plkavg
+    from oracle.disort_rad_np import disort_rad_column
+    rng = np.random.default_rng(300 + seed)
+    nstr = [4, 8, 16, 6][seed]
+    L = int(rng.integers(1, 7))
+    tau = 10 ** rng.uniform(-3, 0.7, L)
+    ssa = rng.uniform(0, 0.99, L)
+    g = rng.uniform(0, 0.8, L)
+    chis = [[gg ** l for l in range(1, nstr + 1)] for gg in g]
+    pmom = np.array([[1.0] + c for c in chis])
+    planck = seed % 2 == 1
+    umu0, fbeam, alb, fisot = rng.uniform(0.1, 1), 1.7, rng.uniform(0, 1), 0.03
+    kw = {}
+    pk, bsurf, btop = None, 0.0, 0.0
+    if planck:
+        temper = np.linspace(180, 290, L + 1)
+        kw = dict(planck=True, temper=temper, btemp=295.0, ttemp=160.0, temis=0.4,
+                  wvnmlo=300.0, wvnmhi=1000.0)
+        pk = np.array([plkavg(300.0, 1000.0, t) for t in temper])
+        bsurf, btop = plkavg(300.0, 1000.0, 295.0), 0.4 * plkavg(300.0, 1000.0, 160.0)
+    taus = np.concatenate([[0.0], np.cumsum(tau)])
+    ut = np.sort(np.concatenate([[0.0, taus[-1]], rng.uniform(0, taus[-1], 3)]))
+    umu = np.array([-0.9, -0.35, 0.2, 0.65, 1.0])
+    r = disort_rad_column(tau, ssa, pmom, nstr, umu=umu, phi=[0.0], utau=ut, umu0=umu0,
+                          fbeam=fbeam, albedo=alb, fisot=fisot, **kw)
+    for m in range(nstr):
+        ops, ip, im, cp, cm = km.solve_mode(tau, ssa, chis, nstr, m, umu0=umu0, fbeam=fbeam,
+                                            albedo=alb, fisot=fisot, pk=pk, bsurf=bsurf,
+                                            btop=btop)
+        ref = r["uum"][m]
+        scale = np.abs(r["uum"][0]).max()
+        for iu, mu in enumerate(umu):
+            got = km.user_radiance(ops, ip, im, cp, cm, nstr, m, mu, ut, umu0=umu0, fbeam=fbeam,
+                                   albedo=alb, fisot=fisot, bsurf=bsurf, btop=btop)
+            err = np.abs(got - ref[:, iu]).max() / scale
+            assert err < 1e-9, (m, mu, got, ref[:, iu])
