@@ -112,6 +112,43 @@ int hd_context_reserve(hd_context *ctx, const hd_config *cfg, long nsolve);
 int hd_solve(hd_context *ctx, const hd_config *cfg, const hd_inputs *in, double *flux,
              int *status, void *stream);
 
+/*
+ * Intensity path (flags usrtau / usrang, onlyfl off): pydisort's forward with
+ * radiances and DisortImpl::get_rad [EXTERNAL], as called at
+ * tests/test_disort.cpp:13-55 (user_mu, user_phi, user_tau; get_rad at :52)
+ * and by the legacy driver src/rtsolver/rt_solver_disort.cpp_:210-286
+ * (c_disort, then ds_out_.uu interpolated onto outgoing rays).  Every
+ * azimuthal mode m < nstr (mode 0 only without a beam), nstr <= 16.
+ *
+ *   utau   HOST [ntau] user optical depths (unscaled, >= 0, ascending);
+ *          ntau = 0: the nlyr+1 layer boundaries of every column
+ *   umu    HOST [numu] user polar cosines, nonzero, > 0 upward
+ *   phi    HOST [nphi] user azimuths [deg]
+ *   phi0   DEVICE [nwave*ncol] beam azimuth [deg] or NULL (0)
+ *   onlyfl 1: fluxes at the user depths only (uu untouched)
+ * Outputs (device):
+ *   flux [nwave][ncol][ntau][2]  index 0 = the deepest user depth (harp order,
+ *        as the level fluxes of hd_solve), [..][0] up, [..][1] rfldir + rfldn
+ *   uu   [nwave][ncol][nphi][ntau][numu]  radiance, user order
+ *        (cdisort's uu[j][lu][iu] per solve)
+ * No Nakajima-Tanaka intensity correction is applied: radiances are the
+ * delta-M solution's (identical where the truncation vanishes, chi_nstr = 0).
+ */
+typedef struct hd_radiance {
+  int ntau;
+  const double *utau;
+  int numu;
+  const double *umu;
+  int nphi;
+  const double *phi;
+  const double *phi0;
+  int onlyfl;
+} hd_radiance;
+
+int hd_solve_radiance(hd_context *ctx, const hd_config *cfg, const hd_inputs *in,
+                      const hd_radiance *rad, double *flux, double *uu, int *status,
+                      void *stream);
+
 /* host helper: the double-Gauss quadrature the kernels use (nstr/2 nodes on (0,1)) */
 int hd_quadrature(int nstr, double *mu, double *w);
 

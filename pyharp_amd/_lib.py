@@ -25,7 +25,7 @@ HD_STATUS_ERROR_MASK = 0x0F
 # every symbol include/hdisort.h declares
 EXPORTED = ("hd_version", "hd_last_error", "hd_context_create", "hd_context_destroy",
             "hd_context_set_chunk", "hd_context_set_timing", "hd_context_get_timing",
-            "hd_context_reserve", "hd_solve", "hd_quadrature")
+            "hd_context_reserve", "hd_solve", "hd_solve_radiance", "hd_quadrature")
 
 # every symbol include/hdharp.h declares (harp-side steps around the solve)
 HARP_EXPORTED = ("hd_attenuate", "hd_band_optics", "hd_band_flux", "hd_heating_rate",
@@ -50,6 +50,11 @@ class HdInputs(ctypes.Structure):
                 ("fbeam", _dp), ("umu0", _dp), ("albedo", _dp), ("btemp", _dp),
                 ("ttemp", _dp), ("temis", _dp), ("fisot", _dp), ("temf", _dp),
                 ("wave_lower", _dp), ("wave_upper", _dp)]
+
+
+class HdRadiance(ctypes.Structure):
+    _fields_ = [("ntau", ctypes.c_int), ("utau", _dp), ("numu", ctypes.c_int), ("umu", _dp),
+                ("nphi", ctypes.c_int), ("phi", _dp), ("phi0", _dp), ("onlyfl", ctypes.c_int)]
 
 
 class HdTiming(ctypes.Structure):
@@ -80,6 +85,10 @@ def load(path: str = LIB_PATH):
     lib.hd_context_reserve.argtypes = [ctypes.c_void_p, ctypes.POINTER(HdConfig), ctypes.c_long]
     lib.hd_solve.argtypes = [ctypes.c_void_p, ctypes.POINTER(HdConfig), ctypes.POINTER(HdInputs),
                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.hd_solve_radiance.argtypes = [ctypes.c_void_p, ctypes.POINTER(HdConfig),
+                                      ctypes.POINTER(HdInputs), ctypes.POINTER(HdRadiance),
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p]
     lib.hd_quadrature.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                   ctypes.POINTER(ctypes.c_double)]
     ci, cd = ctypes.c_int, ctypes.c_double
@@ -145,6 +154,15 @@ class Context:
         rc = load().hd_solve(self.handle, ctypes.byref(cfg), ctypes.byref(inp),
                              ctypes.c_void_p(flux_ptr), ctypes.c_void_p(status_ptr or 0),
                              ctypes.c_void_p(stream_ptr or 0))
+        check(rc, self.handle)
+
+    def solve_radiance(self, cfg: HdConfig, inp: HdInputs, rad: HdRadiance, flux_ptr: int,
+                       uu_ptr: int | None, status_ptr: int | None, stream_ptr: int | None):
+        rc = load().hd_solve_radiance(self.handle, ctypes.byref(cfg), ctypes.byref(inp),
+                                      ctypes.byref(rad), ctypes.c_void_p(flux_ptr),
+                                      ctypes.c_void_p(uu_ptr or 0),
+                                      ctypes.c_void_p(status_ptr or 0),
+                                      ctypes.c_void_p(stream_ptr or 0))
         check(rc, self.handle)
 
 

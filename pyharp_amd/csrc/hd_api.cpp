@@ -19,6 +19,7 @@
 
 #include "../../include/hdisort.h"
 #include "hd_kernels.hpp"
+#include "hd_rad.hpp"
 
 struct hd_context {
   int device = 0;
@@ -43,6 +44,9 @@ struct hd_context {
   hipEvent_t ev_pro[2] = {nullptr, nullptr};  // next chunk's prologue done (side stream)
   hipEvent_t ev_fork = nullptr;                // start of a solve on the caller's stream
   double* sink = nullptr;                      // team kernels: stores of lanes >= nstr/2
+  bool rad_tables = false;                     // intensity-path constants uploaded
+  double* rad_grid = nullptr;                  // device copies of umu | phi | utau
+  size_t rad_grid_len = 0;
 };
 
 namespace {
@@ -283,6 +287,7 @@ int hd_context_destroy(hd_context* ctx) {
   }
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->sink) (void)hipFree(ctx->sink);
+  if (ctx->rad_grid) (void)hipFree(ctx->rad_grid);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   for (auto& e : ctx->pool)
     if (e) (void)hipEventDestroy(e);
@@ -519,6 +524,179 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
       return fail(ctx, HD_ENUMERIC,
                   "hd_solve: at least one solve failed (bad input, eigen breakdown or non-finite "
                   "result); DisortWrapper::Run failed.");
+  }
+  return HD_OK;
+}
+
+int hd_solve_radiance(hd_context* ctx, const hd_config* cfg, const hd_inputs* in,
+                      const hd_radiance* rad, double* flux, double* uu, int* status,
+                      void* stream_) {
+  if (!ctx) return fail(nullptr, HD_EINVAL, "hd_solve_radiance: null context");
+  int rc = validate(ctx, cfg, in, flux);
+  if (rc) return rc;
+  if (!rad) return fail(ctx, HD_EINVAL, "hd_solve_radiance: null radiance config");
+  const int nn = cfg->nstr / 2;
+  if (nn > hd::kRadMaxNN)
+    return fail(ctx, HD_EINVAL, "hd_solve_radiance: nstr=%d; the intensity path supports nstr <= %d",
+                cfg->nstr, 2 * hd::kRadMaxNN);
+  const bool radiances = rad->onlyfl == 0;
+  const int nlyr = cfg->nlyr;
+  const int ntau = rad->ntau > 0 ? rad->ntau : nlyr + 1;
+  const int numu = radiances ? rad->numu : 0;
+  const int nphi = radiances ? rad->nphi : 0;
+  if (rad->ntau < 0 || (rad->ntau > 0 && !rad->utau))
+    return fail(ctx, HD_EINVAL, "hd_solve_radiance: ntau=%d needs utau", rad->ntau);
+  for (int i = 0; i < rad->ntau; ++i)
+    if (!(rad->utau[i] >= 0.0) || (i > 0 && !(rad->utau[i] >= rad->utau[i - 1])))
+      return fail(ctx, HD_EINVAL, "hd_solve_radiance: utau must be >= 0 and ascending");
+  if (radiances) {
+    if (numu < 1 || !rad->umu || nphi < 1 || !rad->phi || !uu)
+      return fail(ctx, HD_EINVAL,
+                  "hd_solve_radiance: radiances need numu >= 1, nphi >= 1, umu, phi and uu");
+    for (int i = 0; i < numu; ++i)
+      if (!(rad->umu[i] != 0.0) || !(std::fabs(rad->umu[i]) <= 1.0))
+        return fail(ctx, HD_EINVAL, "hd_solve_radiance: umu[%d]=%g must be in [-1,0)U(0,1]", i,
+                    rad->umu[i]);
+  }
+  const long nsolve = (long)in->nwave * in->ncol;
+  if (nsolve == 0) return HD_OK;
+  HD_HIP(ctx, hipSetDevice(ctx->device));
+  hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+  const bool planck = (cfg->flags & HD_FLAG_PLANCK) != 0;
+  const bool beam = in->fbeam != nullptr;
+  const bool sync = status == nullptr;
+  const int nm_mode = (radiances && beam) ? cfg->nstr : 1;
+  const int nmom = std::max(0, std::min(cfg->nmom, cfg->nprop - 2));
+
+  rc = ensure_tables(ctx);
+  if (rc) return rc;
+  if (!ctx->rad_tables) {
+    static hd::QuadHost all[hd::kMaxNN];
+    for (int q = 1; q <= hd::kMaxNN; ++q) make_quad(q, all[q - 1]);
+    hipError_t e = hd::upload_rad_tables(all);
+    if (e != hipSuccess)
+      return fail(ctx, HD_EHIP, "hd_solve_radiance: constant upload: %s", hipGetErrorString(e));
+    ctx->rad_tables = true;
+  }
+  // user grid on the device: umu | phi | utau
+  const size_t ngrid = (size_t)numu + nphi + rad->ntau;
+  if (ngrid > ctx->rad_grid_len) {
+    if (ctx->rad_grid) (void)hipFree(ctx->rad_grid);
+    ctx->rad_grid = nullptr;
+    ctx->rad_grid_len = 0;
+    HD_HIP(ctx, hipMalloc(&ctx->rad_grid, ngrid * sizeof(double)));
+    ctx->rad_grid_len = ngrid;
+  }
+  double* d_umu = ctx->rad_grid;
+  double* d_phi = d_umu + numu;
+  double* d_utau = d_phi + nphi;
+  if (numu) HD_HIP(ctx, hipMemcpyAsync(d_umu, rad->umu, numu * sizeof(double), hipMemcpyHostToDevice, stream));
+  if (nphi) HD_HIP(ctx, hipMemcpyAsync(d_phi, rad->phi, nphi * sizeof(double), hipMemcpyHostToDevice, stream));
+  if (rad->ntau)
+    HD_HIP(ctx, hipMemcpyAsync(d_utau, rad->utau, rad->ntau * sizeof(double), hipMemcpyHostToDevice, stream));
+
+  // chunk: scratch per solve = modes x (per-unit records + radiance per mode) + prologue
+  const size_t per_unit = hd::rad_scratch_doubles_per_unit(nn, nlyr) + (size_t)ntau * numu;
+  const size_t per_solve = (size_t)nm_mode * per_unit + (size_t)(nlyr + 1) + nlyr +
+                           (planck ? (size_t)nlyr + 3 : 0);
+  const double budget = 4.0 * 1024.0 * 1024.0 * 1024.0 / 8.0;  // doubles
+  long chunk = std::max<long>(1, std::min<long>(nsolve, (long)(budget / (double)per_solve)));
+  chunk = std::min<long>(chunk, 0x7fffffffL / std::max(1, nm_mode));
+  if (ctx->chunk > 0) chunk = std::min(chunk, ctx->chunk);
+  rc = ensure_scratch(ctx, per_solve * chunk);
+  if (rc) return rc;
+  if (sync) {
+    rc = ensure_status(ctx, (size_t)nsolve);
+    if (rc) return rc;
+    status = ctx->status;
+  }
+  HD_HIP(ctx, hipMemsetAsync(status, 0, sizeof(int) * nsolve, stream));
+  HD_HIP(ctx, hipMemsetAsync(ctx->anyerr, 0, sizeof(int), stream));
+
+  const size_t nuc = (size_t)nm_mode * chunk;  // units of the largest chunk
+  double* q = ctx->scratch;
+  double* r_sw = q;   q += (size_t)nlyr * hd::layer_record_doubles(nn) * nuc;
+  double* r_rd = q;   q += (size_t)nlyr * hd::rad_rec_doubles(nn) * nuc;
+  double* r_bs = q;   q += (size_t)nlyr * hd::rad_bsub_doubles(nn) * nuc;
+  double* r_lev = q;  q += (size_t)(nlyr + 1) * 2 * nn * nuc;
+  double* r_cst = q;  q += (size_t)nlyr * 2 * nn * nuc;
+  double* r_radm = q; q += (size_t)ntau * numu * nuc;
+  double* r_taus = q; q += (size_t)(nlyr + 1) * chunk;
+  double* r_tauc = q; q += (size_t)nlyr * chunk;
+  double* r_planck = planck ? q : nullptr;
+
+  for (long s0 = 0; s0 < nsolve; s0 += chunk) {
+    const int ns = (int)std::min(chunk, nsolve - s0);
+    hd::TaucArgs ta{};
+    ta.prop = in->prop;
+    ta.out = r_tauc;
+    ta.s0 = s0;
+    ta.nsc = ns;
+    ta.nlyr = nlyr;
+    ta.nprop = cfg->nprop;
+    ta.use_f = nmom >= cfg->nstr;
+    ta.f_slot = 1 + cfg->nstr;
+    hd::PlanckArgs pa{};
+    pa.temf = in->temf;
+    pa.btemp = in->btemp;
+    pa.ttemp = in->ttemp;
+    pa.temis = in->temis;
+    pa.wlo = in->wave_lower;
+    pa.whi = in->wave_upper;
+    pa.out = r_planck;
+    pa.s0 = s0;
+    pa.nsc = ns;
+    pa.ncol = in->ncol;
+    pa.nlyr = nlyr;
+    hd::launch_prologue(planck ? &pa : nullptr, beam ? &ta : nullptr, stream);
+    hd::RadArgs a{};
+    a.prop = in->prop;
+    a.fbeam = in->fbeam;
+    a.umu0 = in->umu0;
+    a.albedo = in->albedo;
+    a.fisot = in->fisot;
+    a.phi0 = rad->phi0;
+    a.planckv = r_planck;
+    a.tauc = beam ? r_tauc : nullptr;
+    a.taus = r_taus;
+    a.umu = d_umu;
+    a.phi = d_phi;
+    a.utau = rad->ntau > 0 ? d_utau : nullptr;
+    a.rsw = r_sw;
+    a.rrd = r_rd;
+    a.bsub = r_bs;
+    a.lev = r_lev;
+    a.cst = r_cst;
+    a.radm = r_radm;
+    a.flux = flux;
+    a.uu = uu;
+    a.status = status;
+    a.anyerr = ctx->anyerr;
+    a.s0 = s0;
+    a.ns = ns;
+    a.nm = nm_mode;
+    a.nu = ns * nm_mode;
+    a.ncol = in->ncol;
+    a.nlyr = nlyr;
+    a.nprop = cfg->nprop;
+    a.nmom = nmom;
+    a.planck = planck;
+    a.max_sweeps = 16;
+    a.numu = numu;
+    a.nphi = nphi;
+    a.ntau = ntau;
+    hipError_t e = hd::launch_rad_chunk(nn, a, radiances, stream);
+    if (e != hipSuccess)
+      return fail(ctx, HD_EHIP, "hd_solve_radiance: launch failed: %s", hipGetErrorString(e));
+  }
+  if (sync) {
+    int any = 0;
+    HD_HIP(ctx, hipMemcpyAsync(&any, ctx->anyerr, sizeof(int), hipMemcpyDeviceToHost, stream));
+    HD_HIP(ctx, hipStreamSynchronize(stream));
+    if (any)
+      return fail(ctx, HD_ENUMERIC,
+                  "hd_solve_radiance: at least one solve failed (bad input, eigen breakdown or "
+                  "non-finite result); DisortWrapper::Run failed.");
   }
   return HD_OK;
 }

@@ -1,0 +1,1304 @@
+// hd_rad.hip -- gfx950 kernels of the intensity path: every azimuthal mode,
+// fluxes at user optical depths (usrtau) and radiances at user angles
+// (usrang), nstr <= 16.  One lane owns one (solve, mode m) problem ("unit");
+// units are mode-major inside a chunk (u = m*ns + sl), so a wave's lanes share
+// m and the mode-m Legendre tables are uniform loads.
+//
+//   hd_rad_taus_kernel       unscaled depth of every level (cumsum from the top)
+//   hd_rad_layer_kernel<NN>  per (unit, layer): the flux kernel's layer setup
+//                            with the mode-m table Y_l^m(mu_i), parity split by
+//                            (l+m), beam source x (2 - delta_m0), thermal only at
+//                            m = 0; also keeps L, V, k and the particular
+//                            solution for the radiance kernels  [c_soleig,
+//                            c_upbeam, c_upisot per mode]
+//   hd_rad_sweep_kernel<NN>  per unit: adding sweep (Lambert surface and top
+//                            emission only at m = 0) and back-substitution that
+//                            keeps I+ and I- at every level   [c_setmtx, c_solve0]
+//   hd_rad_const_kernel<NN>  per (unit, layer): the layer's homogeneous
+//                            constants from its level intensities, pivot-free
+//   hd_rad_flux_kernel<NN>   per (solve, user depth): fluxes from the m = 0
+//                            field inside the layer                 [c_fluxes]
+//   hd_rad_user_kernel<NN>   per (unit, user angle): source-function integration
+//                            along the ray through every layer       [c_usrint]
+//   hd_rad_azimuth_kernel    uu = sum_m I_m cos(m (phi - phi0))
+//
+// Formulation: DESIGN.md section 3b, mirrored in numpy by
+// tests/kernel_model_rad.py; oracle: oracle/disort_rad_np.py.
+#include <cmath>
+
+#include "hd_rad.hpp"
+
+namespace hd {
+
+namespace {
+
+constexpr int kLayerBlockR = 256;
+constexpr int kLayersPerBlockR = kLayerBlockR / 64;
+
+template <int NN>
+struct RadTab {
+  double lam[2 * NN][2 * NN][NN];  // Y_l^m(mu_i): [m][l][i]
+};
+
+struct RadConst {
+  Quad<1> q1;
+  Quad<2> q2;
+  Quad<3> q3;
+  Quad<4> q4;
+  Quad<5> q5;
+  Quad<6> q6;
+  Quad<7> q7;
+  Quad<8> q8;
+  RadTab<1> t1;
+  RadTab<2> t2;
+  RadTab<3> t3;
+  RadTab<4> t4;
+  RadTab<5> t5;
+  RadTab<6> t6;
+  RadTab<7> t7;
+  RadTab<8> t8;
+  double seed[2 * kRadMaxNN];                // prod_{i<=m} sqrt((2i-1)/(2i))
+  double ra[2 * kRadMaxNN][2 * kRadMaxNN];   // [m][l] (2l-1)/sqrt(l^2-m^2), l > m
+  double rb[2 * kRadMaxNN][2 * kRadMaxNN];   // [m][l] sqrt((l-1)^2-m^2)/sqrt(l^2-m^2)
+};
+__constant__ RadConst c_rad;
+
+template <int NN>
+__device__ __forceinline__ const Quad<NN>& quad_r() {
+  if constexpr (NN == 1) return c_rad.q1;
+  else if constexpr (NN == 2) return c_rad.q2;
+  else if constexpr (NN == 3) return c_rad.q3;
+  else if constexpr (NN == 4) return c_rad.q4;
+  else if constexpr (NN == 5) return c_rad.q5;
+  else if constexpr (NN == 6) return c_rad.q6;
+  else if constexpr (NN == 7) return c_rad.q7;
+  else return c_rad.q8;
+}
+template <int NN>
+__device__ __forceinline__ const RadTab<NN>& tab_r() {
+  if constexpr (NN == 1) return c_rad.t1;
+  else if constexpr (NN == 2) return c_rad.t2;
+  else if constexpr (NN == 3) return c_rad.t3;
+  else if constexpr (NN == 4) return c_rad.t4;
+  else if constexpr (NN == 5) return c_rad.t5;
+  else if constexpr (NN == 6) return c_rad.t6;
+  else if constexpr (NN == 7) return c_rad.t7;
+  else return c_rad.t8;
+}
+
+// Y_m^m(x) = seed_m (1 - x^2)^(m/2)
+__device__ __forceinline__ double ylm_seed(int m, double x) {
+  const double s = sqrt(fmax(0.0, 1.0 - x * x));
+  double p = c_rad.seed[m];
+  for (int i = 0; i < m; ++i) p *= s;
+  return p;
+}
+
+// Y_l^m(x), l < N (compile-time l, runtime m)
+template <int N>
+__device__ __forceinline__ void ylm_row(int m, double x, double (&y)[N]) {
+  const double seed = ylm_seed(m, x);
+  double y1 = 0.0, y2 = 0.0;
+#pragma unroll
+  for (int l = 0; l < N; ++l) {
+    const double v =
+        l < m ? 0.0 : (l == m ? seed : fma(c_rad.ra[m][l] * x, y1, -c_rad.rb[m][l] * y2));
+    y[l] = v;
+    y2 = y1;
+    y1 = v;
+  }
+}
+
+__device__ __forceinline__ void flag(const RadArgs& A, long s, int st) {
+  if (st) {
+    atomicOr(&A.status[s], st);
+    if (st & 0x0F) atomicOr(A.anyerr, 1);
+  }
+}
+
+// int_{t1}^{t2} a exp(-c (t - tref)) exp(-(t - t1)/mu) dt/mu, t1 = evaluation
+// depth, (t2 - t1)/mu >= 0; the 1 + c mu -> 0 limit through (1 - e^-x)/x
+__device__ __forceinline__ double seg_exp(double a, double c, double t1, double t2, double tref,
+                                          double mu) {
+  const double p1 = exp(-c * (t1 - tref));
+  const double den = fma(c, mu, 1.0);
+  const double dt = (t2 - t1) / mu;
+  const double x = den * dt;
+  if (fabs(x) < 0.5) {
+    const double ph = x == 0.0 ? 1.0 : -expm1(-x) / x;
+    return a * p1 * dt * ph;
+  }
+  const double p2 = exp(-c * (t2 - tref) - dt);
+  return a * (p1 - p2) / den;
+}
+
+// user depth lu of solve sl: the caller's utau or the level depths
+__device__ __forceinline__ double user_tau(const RadArgs& A, int lu, int sl) {
+  return A.utau ? A.utau[lu] : A.taus[(size_t)lu * A.ns + sl];
+}
+
+}  // namespace
+
+// ============================================================================
+// unscaled depth of every level, solver order (0 = top)
+// ============================================================================
+__global__ __launch_bounds__(256) void hd_rad_taus_kernel(RadArgs A) {
+  const int sl = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sl >= A.ns) return;
+  const long s = A.s0 + sl;
+  const int L = A.nlyr, np = A.nprop;
+  const double* p = A.prop + (size_t)s * L * np;
+  double t = 0.0;
+  A.taus[sl] = 0.0;
+  for (int lc = 0; lc < L; ++lc) {
+    t += p[(size_t)(L - 1 - lc) * np];
+    A.taus[(size_t)(lc + 1) * A.ns + sl] = t;
+  }
+  if (A.utau && A.ntau > 0 && A.utau[A.ntau - 1] > t * (1.0 + 1e-12) + 1e-300)
+    flag(A, s, kStBadInput);  // user depth below the bottom
+}
+
+// ============================================================================
+// per-(unit, layer) setup (hd_layer_kernel generalised to mode m)
+// ============================================================================
+template <int NN>
+__global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
+  constexpr int N = 2 * NN;
+  constexpr int kPsi = NN > 1 ? NN * NN : 1;
+  constexpr int nsym = NN * (NN + 1) / 2;
+  __shared__ double psi_lds[kPsi * kLayerBlockR];
+  const Quad<NN>& Qc = quad_r<NN>();
+  const int lt = threadIdx.x;
+  const int ntile = (A.nu + 63) / 64;
+  const int ts = blockIdx.x % ntile;
+  const int tl = blockIdx.x / ntile;
+  const int u = ts * 64 + (lt & 63);
+  const int lc = tl * kLayersPerBlockR + (lt >> 6);
+  const int L = A.nlyr;
+  if (u >= A.nu || lc >= L) return;
+  const int m = u / A.ns;
+  const int sl = u - m * A.ns;
+  const long s = A.s0 + sl;
+  const size_t nu = A.nu;
+  const int nm = A.nmom;
+  const int np = A.nprop;
+  int st = 0;
+
+  const double* q = A.prop + ((size_t)s * L + (L - 1 - lc)) * np;
+  const double tau = q[0];
+  double ssa = np > 1 ? q[1] : 0.0;
+  if (!(tau >= 0.0) || !(ssa >= 0.0) || !(ssa <= 1.0)) st |= kStBadInput;
+  if (ssa == 1.0) ssa = 1.0 - kDither;
+  const double f = nm >= N ? q[1 + N] : 0.0;
+  if (!(f < 1.0)) st |= kStBadInput;
+  const double taup = (1.0 - ssa * f) * tau;
+  const double om = ssa * (1.0 - f) / (1.0 - ssa * f);
+  const double rf = om / (1.0 - f);
+
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
+  const double fb = A.fbeam ? A.fbeam[s] : 0.0;
+  const bool beam = fb > 0.0 && mu0 > 0.0;
+  if (beam && mu0 > 1.0) st |= kStBadInput;
+  const double rmu0 = beam ? 1.0 / mu0 : 0.0;
+  const double mub = beam ? mu0 : 0.0;
+  const bool therm = A.planck && m == 0;
+
+  // ---- mode-m phase matrix even/odd parts (parity of l+m) + beam vectors ----
+  double lch[NN][NN], ap[NN][NN], xs[NN], xd[NN];
+#pragma unroll
+  for (int i = 0; i < NN; ++i) {
+    xs[i] = xd[i] = 0.0;
+#pragma unroll
+    for (int j = i; j < NN; ++j) lch[i][j] = ap[i][j] = 0.0;
+  }
+  {
+    const int mp = m & 1;
+    const double* lam = &tab_r<NN>().lam[m][0][0];
+    const double seed = ylm_seed(m, mub);
+    double y1 = 0.0, y2 = 0.0;  // Y_{l-1}^m(mu0), Y_{l-2}^m(mu0)
+#pragma nounroll
+    for (int l2 = 0; l2 < NN; ++l2) {
+      const int la = 2 * l2, lb = la + 1;
+      const double ya =
+          la < m ? 0.0 : (la == m ? seed : fma(c_rad.ra[m][la] * mub, y1, -c_rad.rb[m][la] * y2));
+      y2 = y1;
+      y1 = ya;
+      const double yb =
+          lb < m ? 0.0 : (lb == m ? seed : fma(c_rad.ra[m][lb] * mub, y1, -c_rad.rb[m][lb] * y2));
+      y2 = y1;
+      y1 = yb;
+      const int le = mp ? lb : la, lo = mp ? la : lb;
+      const double pe0 = mp ? yb : ya, po0 = mp ? ya : yb;
+      const double che = le == 0 ? 1.0 : (le <= nm ? q[1 + le] : 0.0);
+      const double cho = lo == 0 ? 1.0 : (lo <= nm ? q[1 + lo] : 0.0);
+      const double ge = (2 * le + 1) * (che - f) * rf;
+      const double go = (2 * lo + 1) * (cho - f) * rf;
+      const double* te = lam + le * NN;
+      const double* to = lam + lo * NN;
+      double ue[NN], uo[NN];
+#pragma unroll
+      for (int i = 0; i < NN; ++i) {
+        ue[i] = ge * te[i];
+        uo[i] = go * to[i];
+        xs[i] = fma(ue[i], pe0, xs[i]);
+        xd[i] = fma(uo[i], po0, xd[i]);
+      }
+#pragma unroll
+      for (int i = 0; i < NN; ++i)
+#pragma unroll
+        for (int j = i; j < NN; ++j) {
+          ap[i][j] = fma(ue[i], te[j], ap[i][j]);
+          lch[i][j] = fma(uo[i], to[j], lch[i][j]);
+        }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NN; ++i)
+#pragma unroll
+    for (int j = i; j < NN; ++j) {
+      const double diag = (i == j) ? Qc.rmu[i] : 0.0;
+      const double sij = Qc.sd[i] * Qc.sd[j];
+      lch[i][j] = fma(-sij, lch[i][j], diag);
+      ap[i][j] = fma(-sij, ap[i][j], diag);
+    }
+  double rdl[NN];
+  if (!chol_inplace<NN>(lch, rdl)) st |= kStEigen;
+
+  double* rr = A.rrd + (size_t)lc * rad_rec_doubles(NN) * nu + u;
+  constexpr int oV = nsym, oK = nsym + NN * NN, oZp = oK + NN, oZm = oZp + NN, oH = oZm + NN;
+  constexpr int oBt = oH + NN, oSl = oBt + 1, oTp = oSl + 1, oOm = oTp + 1;
+
+  double y2[NN], lxd[NN];
+  const double fb2 = fb * ((m == 0 ? 0.5 : 1.0) / kPi);
+  if (beam) {
+    double y[NN], z[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) y[i] = Qc.sd[i] * (fb2 * xs[i]);
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      double t = 0.0;
+#pragma unroll
+      for (int k = i; k < NN; ++k) t = fma(lch[k][i], y[k], t);
+      z[i] = t;
+    }
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      double t = 0.0;
+#pragma unroll
+      for (int k = 0; k <= i; ++k) t = fma(lch[i][k], z[k], t);
+      y[i] = t;
+    }
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      const double xdi = -fb2 * xd[i];
+      const double rv = fma(-y[i], Qc.rg[i], xdi * rmu0 * Qc.rmu[i]);
+      y2[i] = Qc.g[i] * rv;
+      lxd[i] = Qc.sd[i] * xdi;
+    }
+    lower_solve<NN>(lch, rdl, y2);
+    lower_solve<NN>(lch, rdl, lxd);
+    lower_t_solve<NN>(lch, rdl, lxd);
+  } else {
+#pragma unroll
+    for (int i = 0; i < NN; ++i) y2[i] = lxd[i] = 0.0;
+  }
+  // thermal (m = 0): cvec = dB + 2 (dB/tau') h,  h = W^-1 D^1/2 L^-T L^-1 D^1/2 mu
+  double cvec[NN];
+  double db = 0.0, bsum = 0.0;
+  if (therm) {
+    const double bt = A.planckv[(size_t)(L - lc) * A.ns + sl];
+    const double bb = taup > 0.0 ? A.planckv[(size_t)(L - lc - 1) * A.ns + sl] : bt;
+    db = bb - bt;
+    bsum = bt + bb;
+    const double b1 = taup > 0.0 ? 2.0 * db / taup : 0.0;
+#pragma unroll
+    for (int i = 0; i < NN; ++i) cvec[i] = Qc.sd[i] * Qc.mu[i];
+    lower_solve<NN>(lch, rdl, cvec);
+    lower_t_solve<NN>(lch, rdl, cvec);
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      rr[(oH + i) * nu] = Qc.rg[i] * cvec[i];
+      cvec[i] = fma(b1 * Qc.rg[i], cvec[i], db);
+    }
+    rr[oBt * nu] = bt;
+    rr[oSl * nu] = 0.5 * b1;
+  } else {
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      cvec[i] = 0.0;
+      rr[(oH + i) * nu] = 0.0;
+    }
+    rr[oBt * nu] = 0.0;
+    rr[oSl * nu] = 0.0;
+  }
+  rr[oTp * nu] = taup;
+  rr[oOm * nu] = om;
+  {  // L (packed lower, row-major)
+    int e = 0;
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int k = 0; k <= i; ++k) rr[(e++) * nu] = lch[i][k];
+  }
+
+  double sym[NN][NN];
+#pragma unroll
+  for (int j = 0; j < NN; ++j) {
+    double mcol[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      double t = 0.0;
+#pragma unroll
+      for (int k = j; k < NN; ++k) t = fma(HD_SYM(ap, i, k), lch[k][j], t);
+      mcol[i] = t;
+    }
+#pragma unroll
+    for (int i = 0; i <= j; ++i) {
+      double t = 0.0;
+#pragma unroll
+      for (int k = i; k < NN; ++k) t = fma(lch[k][i], mcol[k], t);
+      sym[i][j] = t;
+    }
+  }
+  double v[NN][NN];
+  jacobi_eig<NN>(sym, v, A.max_sweeps);
+  double kk[NN];
+#pragma unroll
+  for (int j = 0; j < NN; ++j) {
+    const double k2 = sym[j][j];
+    if (!(k2 > 0.0)) st |= kStEigen;
+    kk[j] = sqrt(k2 > 0.0 ? k2 : 0.0);
+    rr[(oK + j) * nu] = kk[j];
+  }
+#pragma unroll
+  for (int i = 0; i < NN; ++i)
+#pragma unroll
+    for (int j = 0; j < NN; ++j) rr[(oV + i * NN + j) * nu] = v[i][j];
+
+  // ---- beam particular solution at the layer top ----
+  double zp[NN], zm[NN];
+  double e0 = 0.0;
+  if (beam) {
+    double tt[NN];
+    const double r2 = rmu0 * rmu0;
+#pragma unroll
+    for (int j = 0; j < NN; ++j) {
+      double t = 0.0;
+#pragma unroll
+      for (int i = 0; i < NN; ++i) t = fma(v[i][j], y2[i], t);
+      double den = fma(-kk[j], kk[j], r2);
+      if (fabs(den) < 1.0e-9 * r2) {
+        st |= kStResonance;
+        den = den < 0.0 ? -1.0e-9 * r2 : 1.0e-9 * r2;
+      }
+      tt[j] = t / den;
+    }
+    double sv[NN], y[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      double t = 0.0;
+#pragma unroll
+      for (int j = 0; j < NN; ++j) t = fma(v[i][j], tt[j], t);
+      y[i] = t;
+    }
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      double t = 0.0;
+#pragma unroll
+      for (int k = 0; k <= i; ++k) t = fma(lch[i][k], y[k], t);
+      sv[i] = Qc.rg[i] * t;
+    }
+#pragma unroll
+    for (int i = 0; i < NN; ++i) y[i] = Qc.sd[i] * Qc.mu[i] * sv[i];
+    lower_solve<NN>(lch, rdl, y);
+    lower_t_solve<NN>(lch, rdl, y);
+    const double tauc = A.tauc[(size_t)lc * A.ns + sl];
+    const double att = 0.5 * exp(-tauc * rmu0);
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      const double dd = Qc.rg[i] * fma(-y[i], rmu0, lxd[i]);
+      zp[i] = (sv[i] + dd) * att;
+      zm[i] = (sv[i] - dd) * att;
+    }
+    e0 = exp(-taup * rmu0);
+  } else {
+#pragma unroll
+    for (int i = 0; i < NN; ++i) zp[i] = zm[i] = 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < NN; ++i) {
+    rr[(oZp + i) * nu] = zp[i];
+    rr[(oZm + i) * nu] = zm[i];
+  }
+
+  // ---- layer operators in the flux-weighted basis (as hd_layer_kernel) ----
+  double dsq[NN], gsq[NN];
+#pragma unroll
+  for (int j = 0; j < NN; ++j) {
+    const double x = kk[j] * taup;
+    const double mm = -expm1(-x);
+    const double th = mm * rcp_nr(2.0 - mm);
+    const double delta = x > 1.0e-8 ? th * rcp_nr(kk[j] > 0.0 ? kk[j] : 1.0) : 0.5 * taup;
+    dsq[j] = sqrt(delta);
+    gsq[j] = sqrt(kk[j] * th);
+  }
+#pragma unroll
+  for (int j = 0; j < NN; ++j) {
+    double x[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) x[i] = v[i][j];
+    lower_t_solve<NN>(lch, rdl, x);
+#pragma unroll
+    for (int i = 0; i < NN; ++i) psi_lds[(i * NN + j) * kLayerBlockR + lt] = x[i] * gsq[j];
+  }
+#pragma unroll
+  for (int i = NN - 1; i >= 0; --i)
+#pragma unroll
+    for (int j = 0; j < NN; ++j) {
+      double t = 0.0;
+#pragma unroll
+      for (int a = 0; a <= i; ++a) t = fma(lch[i][a], v[a][j], t);
+      v[i][j] = t * dsq[j];
+    }
+
+  double* out = A.rsw + (size_t)lc * ne1<NN>() * nu + u;
+  double ga[NN], gb[NN];
+#pragma unroll
+  for (int i = 0; i < NN; ++i) {
+    ga[i] = Qc.g[i] * (cvec[i] - fma(-zp[i], e0, zm[i]));
+    gb[i] = Qc.g[i] * (fma(zp[i], e0, zm[i]) + bsum);
+  }
+  double pvec[NN], qmr[NN][NN];
+  {
+    double hm[NN][NN], rdh[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int j = i; j < NN; ++j) {
+        double t = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < NN; ++k) t = fma(v[k][i], v[k][j], t);
+        hm[i][j] = t;
+      }
+    if (!chol_inplace<NN>(hm, rdh)) st |= kStEigen;
+#pragma unroll
+    for (int r = 0; r < NN; ++r) lower_solve<NN>(hm, rdh, v[r]);
+#pragma unroll
+    for (int i = 0; i < NN; ++i) pvec[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int j = i; j < NN; ++j) {
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < NN; ++k) t = fma(v[i][k], v[j][k], t);
+        qmr[i][j] = t;
+        pvec[i] = fma(t, ga[j], pvec[i]);
+        if (j != i) pvec[j] = fma(t, ga[i], pvec[j]);
+      }
+  }
+  double qp[NN][NN];
+  {
+    double pt_[NN][NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int j = 0; j < NN; ++j) pt_[i][j] = psi_lds[(i * NN + j) * kLayerBlockR + lt];
+    double hp[NN][NN], rdh[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int j = i; j < NN; ++j) {
+        double t = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < NN; ++k) t = fma(pt_[k][i], pt_[k][j], t);
+        hp[i][j] = t;
+      }
+    if (!chol_inplace<NN>(hp, rdh)) st |= kStEigen;
+#pragma unroll
+    for (int r = 0; r < NN; ++r) lower_solve<NN>(hp, rdh, pt_[r]);
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int j = i; j < NN; ++j) {
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < NN; ++k) t = fma(pt_[i][k], pt_[j][k], t);
+        qp[i][j] = -t;
+      }
+  }
+  double qvec[NN];
+#pragma unroll
+  for (int i = 0; i < NN; ++i) {
+    double t = 0.0;
+#pragma unroll
+    for (int j = 0; j < NN; ++j) t = fma(HD_SYM(qp, i, j), gb[j], t);
+    qvec[i] = t;
+  }
+  double chk = 0.0;
+  {
+    int e = 0;
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int j = i; j < NN; ++j) {
+        const double qm = qmr[i][j];
+        const double r = qm + qp[i][j];
+        const double t = ((i == j) ? 1.0 : 0.0) - qm + qp[i][j];
+        out[e * nu] = r;
+        out[(nsym + e) * nu] = t;
+        chk += r + t;
+        ++e;
+      }
+  }
+#pragma unroll
+  for (int i = 0; i < NN; ++i) {
+    const double sp = Qc.g[i] * (zp[i] * (1.0 - e0) - db) + pvec[i] - qvec[i];
+    const double sm = Qc.g[i] * (-zm[i] * (1.0 - e0) + db) - pvec[i] - qvec[i];
+    out[(2 * nsym + i) * nu] = sp;
+    out[(2 * nsym + NN + i) * nu] = sm;
+    chk += sp + sm;
+  }
+  out[(2 * nsym + 2 * NN) * nu] = taup;
+  if (!isfinite(chk + taup)) st |= kStNonFinite;
+  flag(A, s, st);
+}
+
+// ============================================================================
+// per-unit adding sweep + back-substitution keeping I+/I- at every level
+// ============================================================================
+template <int NN>
+__global__ __launch_bounds__(64) void hd_rad_sweep_kernel(RadArgs A) {
+  const Quad<NN>& Qc = quad_r<NN>();
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= A.nu) return;
+  const int m = u / A.ns;
+  const int sl = u - m * A.ns;
+  const long s = A.s0 + sl;
+  const int L = A.nlyr;
+  const size_t nu = A.nu;
+  constexpr int nsym = NN * (NN + 1) / 2;
+  constexpr int NB = rad_bsub_doubles(NN);
+  int st = 0;
+
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
+  const double fb = A.fbeam ? A.fbeam[s] : 0.0;
+  const bool beam = fb > 0.0 && mu0 > 0.0;
+  double alb = A.albedo ? A.albedo[s] : 0.0;
+  if (!(alb >= 0.0) || !(alb <= 1.0)) st |= kStBadInput;
+  double top = A.fisot ? A.fisot[s] : 0.0;
+  double bsurf = 0.0;
+  if (A.planck) {
+    bsurf = A.planckv[(size_t)(L + 1) * A.ns + sl];
+    top += A.planckv[(size_t)(L + 2) * A.ns + sl];
+  }
+  if (m > 0) alb = top = bsurf = 0.0;  // Lambert surface, isotropic top: mode 0 only
+  const double rmu0 = beam ? 1.0 / mu0 : 0.0;
+  const double f0mu0 = (beam && m == 0) ? fb * mu0 : 0.0;
+
+  double ra[NN][NN];
+  double sd[NN];
+#pragma unroll
+  for (int i = 0; i < NN; ++i) {
+    sd[i] = Qc.g[i] * top;
+#pragma unroll
+    for (int j = i; j < NN; ++j) ra[i][j] = 0.0;
+  }
+  double tauc = 0.0;
+  for (int lc = 0; lc < L; ++lc) {
+    const double* lp = A.rsw + (size_t)lc * ne1<NN>() * nu + u;
+    double* bp = A.bsub + (size_t)lc * NB * nu + u;
+    {  // stack above this layer: R_above (packed upper) and S_down
+      int e = 0;
+#pragma unroll
+      for (int i = 0; i < NN; ++i)
+#pragma unroll
+        for (int j = i; j < NN; ++j) bp[(NN * NN + NN + (e++)) * nu] = ra[i][j];
+#pragma unroll
+      for (int i = 0; i < NN; ++i) bp[(NN * NN + NN + nsym + i) * nu] = sd[i];
+    }
+    double rl[NN][NN], spl[NN];
+    {
+      int e = 0;
+#pragma unroll
+      for (int i = 0; i < NN; ++i)
+#pragma unroll
+        for (int j = i; j < NN; ++j) rl[i][j] = lp[(size_t)(e++) * nu];
+#pragma unroll
+      for (int i = 0; i < NN; ++i) spl[i] = lp[(size_t)(2 * nsym + i) * nu];
+    }
+    double am[NN][NN], w1[NN][NN], t1[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int j = 0; j < NN; ++j) am[i][j] = HD_SYM(ra, i, j);
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+#pragma unroll
+      for (int j = 0; j < NN; ++j) {
+        double t = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < NN; ++k) t = fma(-HD_SYM(rl, i, k), am[k][j], t);
+        w1[i][j] = t;
+      }
+      double t = spl[i];
+#pragma unroll
+      for (int k = 0; k < NN; ++k) t = fma(HD_SYM(rl, i, k), sd[k], t);
+      t1[i] = t;
+    }
+#pragma unroll
+    for (int k = 0; k < NN; ++k) {
+      const double piv = w1[k][k];
+      if (!(fabs(piv) > 1.0e-12)) st |= kStPivot;
+      const double rp = rcp_nr(piv);
+      w1[k][k] = rp;
+#pragma unroll
+      for (int i = k + 1; i < NN; ++i) {
+        const double l = w1[i][k] * rp;
+        w1[i][k] = l;
+#pragma unroll
+        for (int j = k + 1; j < NN; ++j) w1[i][j] = fma(-l, w1[k][j], w1[i][j]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int k = 0; k < i; ++k) t1[i] = fma(-w1[i][k], t1[k], t1[i]);
+#pragma unroll
+    for (int i = NN - 1; i >= 0; --i) {
+#pragma unroll
+      for (int k = i + 1; k < NN; ++k) t1[i] = fma(-w1[i][k], t1[k], t1[i]);
+      t1[i] *= w1[i][i];
+    }
+    double uvec[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      double t = sd[i];
+#pragma unroll
+      for (int k = 0; k < NN; ++k) t = fma(am[i][k], t1[k], t);
+      uvec[i] = t;
+      bp[(size_t)(NN * NN + i) * nu] = t1[i];
+    }
+#pragma unroll
+    for (int r = 0; r < NN; ++r) {
+#pragma unroll
+      for (int j = 0; j < NN; ++j) {
+        double t = am[r][j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) t = fma(-am[r][k], w1[k][j], t);
+        am[r][j] = t * w1[j][j];
+      }
+#pragma unroll
+      for (int j = NN - 1; j >= 0; --j) {
+        double t = am[r][j];
+#pragma unroll
+        for (int k = j + 1; k < NN; ++k) t = fma(-am[r][k], w1[k][j], t);
+        am[r][j] = t;
+      }
+    }
+    double tl[NN][NN];
+    {
+      int e = nsym;
+#pragma unroll
+      for (int i = 0; i < NN; ++i)
+#pragma unroll
+        for (int j = i; j < NN; ++j) tl[i][j] = lp[(size_t)(e++) * nu];
+    }
+#pragma unroll
+    for (int j = 0; j < NN; ++j) {
+      double x[NN];
+#pragma unroll
+      for (int i = 0; i < NN; ++i) x[i] = HD_SYM(tl, i, j);
+#pragma unroll
+      for (int i = 0; i < NN; ++i)
+#pragma unroll
+        for (int k = 0; k < i; ++k) x[i] = fma(-w1[i][k], x[k], x[i]);
+#pragma unroll
+      for (int i = NN - 1; i >= 0; --i) {
+#pragma unroll
+        for (int k = i + 1; k < NN; ++k) x[i] = fma(-w1[i][k], x[k], x[i]);
+        x[i] *= w1[i][i];
+      }
+#pragma unroll
+      for (int i = 0; i < NN; ++i) bp[(size_t)(i * NN + j) * nu] = x[i];
+    }
+#pragma unroll
+    for (int r = 0; r < NN; ++r) {
+      double row[NN];
+#pragma unroll
+      for (int j = 0; j < NN; ++j) {
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < NN; ++k) t = fma(am[r][k], HD_SYM(tl, k, j), t);
+        row[j] = t;
+      }
+#pragma unroll
+      for (int j = 0; j < NN; ++j) am[r][j] = row[j];
+    }
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+#pragma unroll
+      for (int j = i; j < NN; ++j) {
+        double t = rl[i][j];
+#pragma unroll
+        for (int k = 0; k < NN; ++k) t = fma(HD_SYM(tl, i, k), am[k][j], t);
+        ra[i][j] = t;
+      }
+      double t = lp[(size_t)(2 * nsym + NN + i) * nu];
+#pragma unroll
+      for (int k = 0; k < NN; ++k) t = fma(HD_SYM(tl, i, k), uvec[k], t);
+      sd[i] = t;
+    }
+    tauc += lp[(size_t)(2 * nsym + 2 * NN) * nu];
+  }
+
+  // ---- Lambertian surface (mode 0): I+ = x for every stream ----
+  double gsd = 0.0, grg = 0.0;
+#pragma unroll
+  for (int i = 0; i < NN; ++i) {
+    gsd += Qc.g[i] * sd[i];
+#pragma unroll
+    for (int j = 0; j < NN; ++j) grg += Qc.g[i] * HD_SYM(ra, i, j) * Qc.g[j];
+  }
+  double esurf = (1.0 - alb) * bsurf;
+  if (beam) esurf += alb * f0mu0 * exp(-tauc * rmu0) / kPi;
+  const double x = (2.0 * alb * gsd + esurf) / (1.0 - 2.0 * alb * grg);
+  double ip[NN];
+  double chk = 0.0;
+  {
+    double* lv = A.lev + (size_t)L * 2 * NN * nu + u;
+#pragma unroll
+    for (int i = 0; i < NN; ++i) ip[i] = Qc.g[i] * x;
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      double t = sd[i];
+#pragma unroll
+      for (int j = 0; j < NN; ++j) t = fma(HD_SYM(ra, i, j), ip[j], t);
+      lv[i * nu] = x;
+      lv[(NN + i) * nu] = t * Qc.rg[i];
+      chk += t;
+    }
+  }
+  // ---- back-substitution bottom -> top ----
+  for (int lc = L - 1; lc >= 0; --lc) {
+    const double* bp = A.bsub + (size_t)lc * NB * nu + u;
+    double nip[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      double t = bp[(size_t)(NN * NN + i) * nu];
+#pragma unroll
+      for (int j = 0; j < NN; ++j) t = fma(bp[(size_t)(i * NN + j) * nu], ip[j], t);
+      nip[i] = t;
+    }
+    double* lv = A.lev + (size_t)lc * 2 * NN * nu + u;
+#pragma unroll
+    for (int i = 0; i < NN; ++i) ip[i] = nip[i];
+    int e = 0;
+    double dn[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) dn[i] = bp[(size_t)(NN * NN + NN + nsym + i) * nu];
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int j = i; j < NN; ++j) {
+        const double r = bp[(size_t)(NN * NN + NN + (e++)) * nu];
+        dn[i] = fma(r, ip[j], dn[i]);
+        if (j != i) dn[j] = fma(r, ip[i], dn[j]);
+      }
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      lv[i * nu] = ip[i] * Qc.rg[i];
+      lv[(NN + i) * nu] = dn[i] * Qc.rg[i];
+      chk += ip[i] + dn[i];
+    }
+  }
+  if (!isfinite(chk)) st |= kStNonFinite;
+  flag(A, s, st);
+}
+
+// ============================================================================
+// per-(unit, layer) homogeneous constants from the level intensities
+//   C+ = (X^-1 s_top + Y^-1 d_top)/2,  C- = (X^-1 s_bot - Y^-1 d_bot)/2
+//   X^-1 = V^T L^-1 diag(g),  Y^-1 = -K^-1 V^T L^T diag(g)
+// ============================================================================
+template <int NN>
+__device__ __forceinline__ void load_layer(const RadArgs& A, int lc, int u, double (&lch)[NN][NN],
+                                           double (&rd)[NN], double (&v)[NN][NN],
+                                           double (&kk)[NN]) {
+  constexpr int nsym = NN * (NN + 1) / 2;
+  const size_t nu = A.nu;
+  const double* rr = A.rrd + (size_t)lc * rad_rec_doubles(NN) * nu + u;
+  int e = 0;
+#pragma unroll
+  for (int i = 0; i < NN; ++i)
+#pragma unroll
+    for (int k = 0; k <= i; ++k) lch[i][k] = rr[(e++) * nu];
+#pragma unroll
+  for (int i = 0; i < NN; ++i) rd[i] = 1.0 / lch[i][i];
+#pragma unroll
+  for (int i = 0; i < NN; ++i)
+#pragma unroll
+    for (int j = 0; j < NN; ++j) v[i][j] = rr[(nsym + i * NN + j) * nu];
+#pragma unroll
+  for (int j = 0; j < NN; ++j) kk[j] = rr[(nsym + NN * NN + j) * nu];
+}
+
+template <int NN>
+__global__ __launch_bounds__(256) void hd_rad_const_kernel(RadArgs A) {
+  const Quad<NN>& Qc = quad_r<NN>();
+  const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (long)A.nu * A.nlyr) return;
+  const int lc = (int)(id / A.nu);
+  const int u = (int)(id - (long)lc * A.nu);
+  const int m = u / A.ns;
+  const int sl = u - m * A.ns;
+  const long s = A.s0 + sl;
+  const size_t nu = A.nu;
+  constexpr int nsym = NN * (NN + 1) / 2;
+  constexpr int oZp = nsym + NN * NN + NN, oZm = oZp + NN, oH = oZm + NN, oBt = oH + NN;
+  double lch[NN][NN], rd[NN], v[NN][NN], kk[NN];
+  load_layer<NN>(A, lc, u, lch, rd, v, kk);
+  const double* rr = A.rrd + (size_t)lc * rad_rec_doubles(NN) * nu + u;
+  const double bt = rr[oBt * nu], slope = rr[(oBt + 1) * nu], taup = rr[(oBt + 2) * nu];
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
+  const double fb = A.fbeam ? A.fbeam[s] : 0.0;
+  const double rmu0 = (fb > 0.0 && mu0 > 0.0) ? 1.0 / mu0 : 0.0;
+  double cp[NN], cm[NN];
+#pragma unroll
+  for (int side = 0; side < 2; ++side) {  // 0: layer top, 1: layer bottom
+    const double t = side ? taup : 0.0;
+    const double eb = exp(-t * rmu0);
+    const double b2 = 2.0 * fma(slope, t, bt);
+    const double* lv = A.lev + (size_t)(lc + side) * 2 * NN * nu + u;
+    double xs[NN], yd[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      const double ipl = lv[i * nu], imi = lv[(NN + i) * nu];
+      const double zp = rr[(oZp + i) * nu], zm = rr[(oZm + i) * nu], h = rr[(oH + i) * nu];
+      xs[i] = Qc.g[i] * (ipl + imi - (zp + zm) * eb - b2);
+      yd[i] = Qc.g[i] * (ipl - imi - (zp - zm) * eb - 2.0 * slope * h);
+    }
+    lower_solve<NN>(lch, rd, xs);
+    double ly[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {  // L^T yd
+      double a = 0.0;
+#pragma unroll
+      for (int k = i; k < NN; ++k) a = fma(lch[k][i], yd[k], a);
+      ly[i] = a;
+    }
+#pragma unroll
+    for (int j = 0; j < NN; ++j) {
+      double a = 0.0, b = 0.0;
+#pragma unroll
+      for (int i = 0; i < NN; ++i) {
+        a = fma(v[i][j], xs[i], a);
+        b = fma(v[i][j], ly[i], b);
+      }
+      b = kk[j] > 0.0 ? -b / kk[j] : 0.0;
+      if (side == 0) cp[j] = 0.5 * (a + b);
+      else cm[j] = 0.5 * (a - b);
+    }
+  }
+  double* co = A.cst + (size_t)lc * 2 * NN * nu + u;
+#pragma unroll
+  for (int j = 0; j < NN; ++j) {
+    co[j * nu] = cp[j];
+    co[(NN + j) * nu] = cm[j];
+  }
+}
+
+// ============================================================================
+// fluxes at the user depths from the m = 0 field (unit u = sl)
+// ============================================================================
+template <int NN>
+__global__ __launch_bounds__(256) void hd_rad_flux_kernel(RadArgs A) {
+  const Quad<NN>& Qc = quad_r<NN>();
+  const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (long)A.ns * A.ntau) return;
+  const int lu = (int)(id / A.ns);
+  const int sl = (int)(id - (long)lu * A.ns);
+  const int u = sl;  // mode 0
+  const long s = A.s0 + sl;
+  const int L = A.nlyr;
+  const size_t nu = A.nu;
+  constexpr int nsym = NN * (NN + 1) / 2;
+  constexpr int oZp = nsym + NN * NN + NN, oZm = oZp + NN, oH = oZm + NN, oBt = oH + NN;
+  const double tu = user_tau(A, lu, sl);
+  int lc = 0;
+  while (lc < L - 1 && tu > A.taus[(size_t)(lc + 1) * A.ns + sl]) ++lc;
+  const double ttop = A.taus[(size_t)lc * A.ns + sl];
+  const double tau = A.taus[(size_t)(lc + 1) * A.ns + sl] - ttop;
+  double lch[NN][NN], rd[NN], v[NN][NN], kk[NN];
+  load_layer<NN>(A, lc, u, lch, rd, v, kk);
+  const double* rr = A.rrd + (size_t)lc * rad_rec_doubles(NN) * nu + u;
+  const double bt = rr[oBt * nu], slope = rr[(oBt + 1) * nu], taup = rr[(oBt + 2) * nu];
+  const double scale = tau > 0.0 ? taup / tau : 0.0;
+  const double t = fmin(fmax((tu - ttop) * scale, 0.0), taup);
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
+  const double fb = A.fbeam ? A.fbeam[s] : 0.0;
+  const bool beam = fb > 0.0 && mu0 > 0.0;
+  const double rmu0 = beam ? 1.0 / mu0 : 0.0;
+  const double* co = A.cst + (size_t)lc * 2 * NN * nu + u;
+  double al[NN], be[NN];
+#pragma unroll
+  for (int j = 0; j < NN; ++j) {
+    const double a = co[j * nu] * exp(-kk[j] * t);
+    const double b = co[(NN + j) * nu] * exp(-kk[j] * (taup - t));
+    al[j] = a + b;
+    be[j] = kk[j] * (a - b);
+  }
+  double gs[NN], gd[NN];
+#pragma unroll
+  for (int i = 0; i < NN; ++i) {  // V al, V (k be)
+    double a = 0.0, b = 0.0;
+#pragma unroll
+    for (int j = 0; j < NN; ++j) {
+      a = fma(v[i][j], al[j], a);
+      b = fma(v[i][j], be[j], b);
+    }
+    gs[i] = a;
+    gd[i] = b;
+  }
+#pragma unroll
+  for (int i = NN - 1; i >= 0; --i) {  // gs <- L gs (rows bottom-up, in place)
+    double a = 0.0;
+#pragma unroll
+    for (int k = 0; k <= i; ++k) a = fma(lch[i][k], gs[k], a);
+    gs[i] = a;
+  }
+  lower_t_solve<NN>(lch, rd, gd);  // g (I+ - I-)_hom = -L^-T V K be
+  const double eb = exp(-t * rmu0);
+  const double bb = fma(slope, t, bt);
+  double up = 0.0, dn = 0.0;
+#pragma unroll
+  for (int i = 0; i < NN; ++i) {
+    const double zp = rr[(oZp + i) * nu], zm = rr[(oZm + i) * nu], h = rr[(oH + i) * nu];
+    const double ipl = 0.5 * (gs[i] - gd[i]) + Qc.g[i] * (zp * eb + bb + slope * h);
+    const double imi = 0.5 * (gs[i] + gd[i]) + Qc.g[i] * (zm * eb + bb - slope * h);
+    up = fma(Qc.g[i], ipl, up);
+    dn = fma(Qc.g[i], imi, dn);
+  }
+  up *= 2.0 * kPi;
+  dn *= 2.0 * kPi;
+  if (beam) dn += fb * mu0 * exp(-(A.tauc[(size_t)lc * A.ns + sl] + t) * rmu0);
+  double* fo = A.flux + ((size_t)s * A.ntau + (A.ntau - 1 - lu)) * 2;
+  fo[0] = up;
+  fo[1] = dn;
+  if (!isfinite(up + dn)) flag(A, s, kStNonFinite);
+}
+
+// ============================================================================
+// per-(unit, user angle) source-function integration along the ray
+// ============================================================================
+template <int NN>
+__global__ __launch_bounds__(64) void hd_rad_user_kernel(RadArgs A) {
+  constexpr int N = 2 * NN;
+  constexpr int nsym = NN * (NN + 1) / 2;
+  constexpr int oZp = nsym + NN * NN + NN, oZm = oZp + NN, oH = oZm + NN, oBt = oH + NN;
+  const Quad<NN>& Qc = quad_r<NN>();
+  const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (long)A.nu * A.numu) return;
+  const int iu = (int)(id / A.nu);
+  const int u = (int)(id - (long)iu * A.nu);
+  const int m = u / A.ns;
+  const int sl = u - m * A.ns;
+  const long s = A.s0 + sl;
+  const int L = A.nlyr, np = A.nprop, nm = A.nmom;
+  const size_t nu = A.nu;
+  const double muu = A.umu[iu];
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
+  const double fb = A.fbeam ? A.fbeam[s] : 0.0;
+  const bool beam = fb > 0.0 && mu0 > 0.0;
+  const double rmu0 = beam ? 1.0 / mu0 : 0.0;
+  const bool therm = A.planck && m == 0;
+  const double fac = (m == 0 ? 1.0 : 2.0) * fb / (4.0 * kPi);
+  double yu[N], y0[N];
+  ylm_row<N>(m, muu, yu);
+  ylm_row<N>(m, beam ? mu0 : 0.0, y0);
+#pragma unroll
+  for (int l = 0; l < N; ++l) y0[l] = ((l + m) & 1) ? -y0[l] : y0[l];  // Y_l^m(-mu0)
+  const double* lam = &tab_r<NN>().lam[m][0][0];
+  const bool up = muu > 0.0;
+
+  double cur;
+  if (up) {
+    cur = 0.0;
+    if (m == 0) {
+      const double* lv = A.lev + (size_t)L * 2 * NN * nu + u;
+      double fdn = 0.0;
+#pragma unroll
+      for (int i = 0; i < NN; ++i) fdn = fma(Qc.g[i] * Qc.g[i], lv[(NN + i) * nu], fdn);
+      fdn *= 2.0 * kPi;
+      const double alb = A.albedo ? A.albedo[s] : 0.0;
+      if (beam) {
+        const double tb = A.tauc[(size_t)(L - 1) * A.ns + sl] +
+                          A.rrd[((size_t)(L - 1) * rad_rec_doubles(NN) + oBt + 2) * nu + u];
+        fdn += fb * mu0 * exp(-tb * rmu0);
+      }
+      cur = alb / kPi * fdn + (A.planck ? (1.0 - alb) * A.planckv[(size_t)(L + 1) * A.ns + sl]
+                                        : 0.0);
+    }
+  } else {
+    cur = 0.0;
+    if (m == 0) {
+      cur = A.fisot ? A.fisot[s] : 0.0;
+      if (A.planck) cur += A.planckv[(size_t)(L + 2) * A.ns + sl];
+    }
+  }
+  int k = up ? A.ntau - 1 : 0;
+  double chk = 0.0;
+  for (int step = 0; step < L; ++step) {
+    const int lc = up ? L - 1 - step : step;
+    const double ttop = A.taus[(size_t)lc * A.ns + sl];
+    const double tbot = A.taus[(size_t)(lc + 1) * A.ns + sl];
+    // ---- delta-M moments of this layer, mode-m phase row at muu ----
+    const double* q = A.prop + ((size_t)s * L + (L - 1 - lc)) * np;
+    double ssa = np > 1 ? q[1] : 0.0;
+    if (ssa == 1.0) ssa = 1.0 - kDither;
+    const double f = nm >= N ? q[1 + N] : 0.0;
+    const double om = ssa * (1.0 - f) / (1.0 - ssa * f);
+    const double rf = om / (1.0 - f);
+    double cue[NN], cuo[NN];
+    double x0 = 0.0;
+#pragma unroll
+    for (int i = 0; i < NN; ++i) cue[i] = cuo[i] = 0.0;
+#pragma unroll
+    for (int l = 0; l < N; ++l) {
+      const double chi = l == 0 ? 1.0 : (l <= nm ? q[1 + l] : 0.0);
+      const double gl = (2 * l + 1) * (chi - f) * rf;
+      const double t = 0.5 * gl * yu[l];
+      x0 = fma(gl * yu[l], y0[l], x0);
+      const bool ev = ((l + m) & 1) == 0;
+      const double te = ev ? t : 0.0, to = ev ? 0.0 : t;
+#pragma unroll
+      for (int i = 0; i < NN; ++i) {
+        const double p = lam[l * NN + i];
+        cue[i] = fma(te, p, cue[i]);
+        cuo[i] = fma(to, p, cuo[i]);
+      }
+    }
+    double lch[NN][NN], rd[NN], v[NN][NN], kk[NN];
+    load_layer<NN>(A, lc, u, lch, rd, v, kk);
+    const double* rr = A.rrd + (size_t)lc * rad_rec_doubles(NN) * nu + u;
+    const double bt = rr[oBt * nu], slope = rr[(oBt + 1) * nu], taup = rr[(oBt + 2) * nu];
+    // ce = V^T L^T (sd cue), co = -k V^T L^-1 (sd cuo)
+    double a1[NN], b1[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) b1[i] = Qc.sd[i] * cuo[i];
+    lower_solve<NN>(lch, rd, b1);
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      double a = 0.0;
+#pragma unroll
+      for (int kx = i; kx < NN; ++kx) a = fma(lch[kx][i], Qc.sd[kx] * cue[kx], a);
+      a1[i] = a;
+    }
+    const double* co = A.cst + (size_t)lc * 2 * NN * nu + u;
+    double hpl[NN], hmi[NN];
+#pragma unroll
+    for (int j = 0; j < NN; ++j) {
+      double ce = 0.0, cx = 0.0;
+#pragma unroll
+      for (int i = 0; i < NN; ++i) {
+        ce = fma(v[i][j], a1[i], ce);
+        cx = fma(v[i][j], b1[i], cx);
+      }
+      cx *= -kk[j];
+      hpl[j] = co[j * nu] * (ce + cx);
+      hmi[j] = co[(NN + j) * nu] * (ce - cx);
+    }
+    double ab = 0.0, a0 = 0.0, a1t = 0.0;
+    if (beam) {
+      double sc = 0.0;
+#pragma unroll
+      for (int i = 0; i < NN; ++i) {
+        const double zp = rr[(oZp + i) * nu], zm = rr[(oZm + i) * nu];
+        sc = fma(Qc.w[i], fma(cue[i], zp + zm, cuo[i] * (zp - zm)), sc);
+      }
+      ab = fma(fac * x0, exp(-A.tauc[(size_t)lc * A.ns + sl] * rmu0), sc);
+    }
+    if (therm) {
+      double we = 0.0, wo = 0.0;
+#pragma unroll
+      for (int i = 0; i < NN; ++i) {
+        we = fma(Qc.w[i], cue[i], we);
+        wo = fma(Qc.w[i] * cuo[i], rr[(oH + i) * nu], wo);
+      }
+      const double ce0 = (1.0 - om) + 2.0 * we;
+      a1t = slope * ce0;
+      a0 = fma(bt, ce0, 2.0 * slope * wo);
+    }
+    auto integ = [&](double t1, double t2) {
+      double r = 0.0;
+#pragma unroll
+      for (int j = 0; j < NN; ++j) {
+        r += seg_exp(hpl[j], kk[j], t1, t2, 0.0, muu);
+        r += seg_exp(hmi[j], -kk[j], t1, t2, taup, muu);
+      }
+      if (beam) r += seg_exp(ab, rmu0, t1, t2, 0.0, muu);
+      if (therm) {
+        const double e2 = exp(-(t2 - t1) / muu);
+        r += (a0 + a1t * t1 + a1t * muu) - (a0 + a1t * t2 + a1t * muu) * e2;
+      }
+      return r;
+    };
+    const double tau = tbot - ttop;
+    const double scale = tau > 0.0 ? taup / tau : 0.0;
+    const double tfar = up ? taup : 0.0;
+    if (up) {
+      while (k >= 0 && user_tau(A, k, sl) >= ttop) {
+        const double t = fmin(fmax((user_tau(A, k, sl) - ttop) * scale, 0.0), taup);
+        const double val = cur * exp(-(tfar - t) / muu) + integ(t, tfar);
+        A.radm[((size_t)k * A.numu + iu) * nu + u] = val;
+        chk += val;
+        --k;
+      }
+      cur = cur * exp(-taup / muu) + integ(0.0, taup);
+    } else {
+      while (k < A.ntau && user_tau(A, k, sl) <= tbot) {
+        const double t = fmin(fmax((user_tau(A, k, sl) - ttop) * scale, 0.0), taup);
+        const double val = cur * exp(t / muu) + integ(t, 0.0);
+        A.radm[((size_t)k * A.numu + iu) * nu + u] = val;
+        chk += val;
+        ++k;
+      }
+      cur = cur * exp(taup / muu) + integ(taup, 0.0);
+    }
+  }
+  // user depths beyond the bottom (flagged by the taus kernel): bottom value
+  for (; k < A.ntau && !up; ++k) A.radm[((size_t)k * A.numu + iu) * nu + u] = cur;
+  if (!isfinite(chk)) flag(A, s, kStNonFinite);
+}
+
+// ============================================================================
+// uu[s][j][lu][iu] = sum_m I_m cos(m (phi_j - phi0))
+// ============================================================================
+__global__ __launch_bounds__(256) void hd_rad_azimuth_kernel(RadArgs A) {
+  const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long n = (long)A.ns * A.nphi * A.ntau * A.numu;
+  if (id >= n) return;
+  const int sl = (int)(id % A.ns);
+  long r = id / A.ns;
+  const int iu = (int)(r % A.numu);
+  r /= A.numu;
+  const int lu = (int)(r % A.ntau);
+  const int j = (int)(r / A.ntau);
+  const long s = A.s0 + sl;
+  const double ph0 = A.phi0 ? A.phi0[s] : 0.0;
+  const double dphi = (A.phi[j] - ph0) * (kPi / 180.0);
+  const double* src = A.radm + ((size_t)lu * A.numu + iu) * A.nu + sl;
+  double acc = 0.0;
+  for (int m = 0; m < A.nm; ++m) acc = fma(src[(size_t)m * A.ns], cos(m * dphi), acc);
+  A.uu[(((size_t)s * A.nphi + j) * A.ntau + lu) * A.numu + iu] = acc;
+}
+
+// ============================================================================
+// host side
+// ============================================================================
+template <int NN>
+static void fill_rad(Quad<NN>& q, RadTab<NN>& t, const QuadHost& h) {
+  for (int i = 0; i < NN; ++i) {
+    q.mu[i] = h.mu[i];
+    q.w[i] = h.w[i];
+    q.sd[i] = h.sd[i];
+    q.g[i] = h.g[i];
+    q.rmu[i] = 1.0 / h.mu[i];
+    q.rg[i] = 1.0 / h.g[i];
+    for (int l = 0; l < 2 * NN; ++l) q.pt[l][i] = h.pt[l][i];
+  }
+  // Y_l^m(mu_i) by the same recurrence as ylm_row
+  for (int m = 0; m < 2 * NN; ++m)
+    for (int i = 0; i < NN; ++i) {
+      const double x = h.mu[i];
+      double seed = 1.0;
+      for (int a = 1; a <= m; ++a) seed *= std::sqrt((2.0 * a - 1) / (2.0 * a));
+      seed *= std::pow(std::sqrt(std::fmax(0.0, 1.0 - x * x)), m);
+      double y1 = 0.0, y2 = 0.0;
+      for (int l = 0; l < 2 * NN; ++l) {
+        double v = 0.0;
+        if (l == m) v = seed;
+        else if (l > m)
+          v = ((2.0 * l - 1) * x * y1 - std::sqrt((double)(l - 1) * (l - 1) - (double)m * m) * y2) /
+              std::sqrt((double)l * l - (double)m * m);
+        t.lam[m][l][i] = v;
+        y2 = y1;
+        y1 = v;
+      }
+    }
+}
+
+hipError_t upload_rad_tables(const QuadHost* per_nn) {
+  static RadConst c;  // ~60 KB: keep off the stack
+  fill_rad<1>(c.q1, c.t1, per_nn[0]);
+  fill_rad<2>(c.q2, c.t2, per_nn[1]);
+  fill_rad<3>(c.q3, c.t3, per_nn[2]);
+  fill_rad<4>(c.q4, c.t4, per_nn[3]);
+  fill_rad<5>(c.q5, c.t5, per_nn[4]);
+  fill_rad<6>(c.q6, c.t6, per_nn[5]);
+  fill_rad<7>(c.q7, c.t7, per_nn[6]);
+  fill_rad<8>(c.q8, c.t8, per_nn[7]);
+  for (int m = 0; m < 2 * kRadMaxNN; ++m) {
+    double sd = 1.0;
+    for (int a = 1; a <= m; ++a) sd *= std::sqrt((2.0 * a - 1) / (2.0 * a));
+    c.seed[m] = sd;
+    for (int l = 0; l < 2 * kRadMaxNN; ++l) {
+      if (l > m) {
+        const double den = std::sqrt((double)l * l - (double)m * m);
+        c.ra[m][l] = (2.0 * l - 1) / den;
+        c.rb[m][l] = std::sqrt((double)(l - 1) * (l - 1) - (double)m * m) / den;
+      } else {
+        c.ra[m][l] = c.rb[m][l] = 0.0;
+      }
+    }
+  }
+  return hipMemcpyToSymbol(HIP_SYMBOL(c_rad), &c, sizeof(RadConst));
+}
+
+template <int NN>
+static void launch_rad(const RadArgs& a, bool radiances, hipStream_t st) {
+  const unsigned ns_b = (unsigned)((a.ns + 255) / 256);
+  hipLaunchKernelGGL(hd_rad_taus_kernel, dim3(ns_b), dim3(256), 0, st, a);
+  const unsigned nb1 = (unsigned)(((a.nu + 63) / 64) *
+                                  ((a.nlyr + kLayersPerBlockR - 1) / kLayersPerBlockR));
+  hipLaunchKernelGGL(hd_rad_layer_kernel<NN>, dim3(nb1), dim3(kLayerBlockR), 0, st, a);
+  hipLaunchKernelGGL(hd_rad_sweep_kernel<NN>, dim3((unsigned)((a.nu + 63) / 64)), dim3(64), 0, st,
+                     a);
+  const long nc = (long)a.nu * a.nlyr;
+  hipLaunchKernelGGL(hd_rad_const_kernel<NN>, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0,
+                     st, a);
+  const long nf = (long)a.ns * a.ntau;
+  hipLaunchKernelGGL(hd_rad_flux_kernel<NN>, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, st,
+                     a);
+  if (radiances && a.numu > 0 && a.nphi > 0) {
+    const long nr = (long)a.nu * a.numu;
+    hipLaunchKernelGGL(hd_rad_user_kernel<NN>, dim3((unsigned)((nr + 63) / 64)), dim3(64), 0, st,
+                       a);
+    const long na = (long)a.ns * a.nphi * a.ntau * a.numu;
+    hipLaunchKernelGGL(hd_rad_azimuth_kernel, dim3((unsigned)((na + 255) / 256)), dim3(256), 0,
+                       st, a);
+  }
+}
+
+hipError_t launch_rad_chunk(int nn, const RadArgs& a, bool radiances, hipStream_t stream) {
+  switch (nn) {
+    case 1: launch_rad<1>(a, radiances, stream); break;
+    case 2: launch_rad<2>(a, radiances, stream); break;
+    case 3: launch_rad<3>(a, radiances, stream); break;
+    case 4: launch_rad<4>(a, radiances, stream); break;
+    case 5: launch_rad<5>(a, radiances, stream); break;
+    case 6: launch_rad<6>(a, radiances, stream); break;
+    case 7: launch_rad<7>(a, radiances, stream); break;
+    case 8: launch_rad<8>(a, radiances, stream); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+size_t rad_scratch_doubles_per_unit(int nn, int nlyr) {
+  const size_t ne1r = (size_t)(nn * (nn + 1) + 2 * nn + 1);
+  return (size_t)nlyr * (ne1r + rad_rec_doubles(nn) + rad_bsub_doubles(nn) + 4 * nn) +
+         (size_t)2 * nn;
+}
+
+}  // namespace hd

@@ -16,6 +16,13 @@ Returns ``flux`` (nwave, ncol, nlyr+1, 2): level 0 = surface, [...,0] upward,
 [...,1] downward (rfldir + rfldn).  CPU tensors are staged through the GPU and
 the result is returned on the input's device; CUDA tensors stay on device.
 
+Intensity path (``tests/test_disort.cpp:13-55``): without ``onlyfl`` the module
+also computes radiances -- at ``user_mu`` x ``user_phi`` with ``usrang``, else at
+the quadrature cosines and ``user_phi`` (default [0]) -- at ``user_tau`` with
+``usrtau`` (else at the level depths); ``get_rad()`` returns them as
+(nwave, ncol, nphi, ntau, numu).  With ``usrtau`` the fluxes are at the user
+depths, (nwave, ncol, ntau, 2), index 0 = the deepest.  nstr <= 16 there.
+
 The arithmetic runs in libhdisort.so (HIP, gfx950) through the C-ABI in
 include/hdisort.h.  There is no CPU fallback: without a HIP device or without
 the built library, ``forward`` raises.
@@ -37,7 +44,7 @@ _KNOWN_FLAGS = {
     "print-transmissivity", "print-phase-function", "deltam", "lyrcut", "ibcnd",
 }
 _BC_KEYS = ("fbeam", "umu0", "albedo", "btemp", "ttemp", "temis", "fisot")
-_BC_IGNORED = ("phi0",)  # azimuth of the beam: no effect on m=0 fluxes
+_BC_IGNORED = ("phi0",)  # azimuth of the beam: used by the radiances only
 
 
 class _DisortState:
@@ -133,13 +140,49 @@ class Disort(RTSolver):
         if self.planck:
             if len(op.wave_lower()) != op.nwave() or len(op.wave_upper()) != op.nwave():
                 raise RuntimeError("Disort: planck needs wave_lower/wave_upper of size nwave")
+        # intensity path: radiances (onlyfl off) and/or fluxes at user depths
+        self.onlyfl = "onlyfl" in flags
+        self.usrtau = "usrtau" in flags
+        self.usrang = "usrang" in flags
+        self.radiance = (not self.onlyfl) or self.usrtau
+        self._rad = None
+        if self.radiance:
+            if ds.nstr > 16:
+                raise RuntimeError(f"Disort: nstr={ds.nstr}; radiances / user depths need "
+                                   "nstr <= 16")
+            if self.usrtau:
+                ut = [float(x) for x in op.user_tau()]
+                if not ut:
+                    raise RuntimeError("Disort: usrtau set but user_tau is empty")
+                if any(x < 0 for x in ut) or any(b < a for a, b in zip(ut, ut[1:])):
+                    raise RuntimeError("Disort: user_tau must be >= 0 and ascending")
+                ds.utau = ut
+                ds.ntau = len(ut)
+            else:
+                ds.utau = []
+                ds.ntau = ds.nlyr + 1
+            if self.usrang:
+                umu = [float(x) for x in op.user_mu()]
+                if not umu or any(x == 0 or abs(x) > 1 for x in umu):
+                    raise RuntimeError("Disort: usrang needs user_mu in [-1,0)U(0,1]")
+            else:
+                mu, _ = _lib.quadrature(ds.nstr) if _lib_loaded() else _gauss(ds.nstr)
+                umu = [-x for x in reversed(mu)] + list(mu)
+            phi = [float(x) for x in op.user_phi()] or [0.0]
+            self._umu, self._phi = umu, phi
+            ds.numu, ds.nphi = (len(umu), len(phi)) if not self.onlyfl else (0, 0)
 
     def ds(self):
         return self.options.ds()
 
-    def get_rad(self, *args, **kwargs):
-        raise NotImplementedError("Disort.get_rad: the intensity path (usrang/usrtau "
-                                  "radiances) is not part of this flux-only solver")
+    def get_rad(self, *args, **kwargs) -> torch.Tensor:
+        """Radiances of the last forward, (nwave, ncol, nphi, ntau, numu)
+        (pydisort DisortImpl::get_rad, tests/test_disort.cpp:52)."""
+        if self.onlyfl:
+            raise RuntimeError("Disort.get_rad: radiances are off (onlyfl flag)")
+        if self._rad is None:
+            raise RuntimeError("Disort.get_rad: call forward first")
+        return self._rad
 
     # ------------------------------------------------------------------ #
     def forward(self, prop: torch.Tensor, bc: Optional[Dict[str, torch.Tensor]] = None,
@@ -198,13 +241,14 @@ class Disort(RTSolver):
                                torch.tensor(op.wave_upper(), dtype=f64, device=dev))
             wl, wu = self._waves[1], self._waves[2]
             keep += [tf, wl, wu]
+        nlev = ds.ntau if self.radiance else nlyr + 1
         if out is None:
-            flux = torch.empty((nwave, ncol, nlyr + 1, 2), dtype=f64, device=dev)
+            flux = torch.empty((nwave, ncol, nlev, 2), dtype=f64, device=dev)
         else:
             if (out.device != dev or out.dtype != f64 or not out.is_contiguous()
-                    or tuple(out.shape) != (nwave, ncol, nlyr + 1, 2)):
+                    or tuple(out.shape) != (nwave, ncol, nlev, 2)):
                 raise RuntimeError("Disort.forward: out must be a contiguous float64 tensor "
-                                   f"of shape {(nwave, ncol, nlyr + 1, 2)} on {dev}")
+                                   f"of shape {(nwave, ncol, nlev, 2)} on {dev}")
             flux = out
         if status is not None and (status.device != dev or status.dtype != torch.int32
                                    or not status.is_contiguous()
@@ -225,11 +269,57 @@ class Disort(RTSolver):
                             fisot=ptr(bct.get("fisot")), temf=ptr(tf), wave_lower=ptr(wl),
                             wave_upper=ptr(wu))
         stream = torch.cuda.current_stream(dev)
-        with torch.cuda.device(dev):
-            _context(dev.index).solve(cfg, inp, flux.data_ptr(),
-                                      status.data_ptr() if status is not None else None,
-                                      stream.cuda_stream)
+        if self.radiance:
+            self._forward_radiance(cfg, inp, flux, status, stream, bc, dev, keep, nwave, ncol)
+        else:
+            with torch.cuda.device(dev):
+                _context(dev.index).solve(cfg, inp, flux.data_ptr(),
+                                          status.data_ptr() if status is not None else None,
+                                          stream.cuda_stream)
         del keep
+        if self._rad is not None and in_dev.type != "cuda":
+            self._rad = self._rad.to(in_dev)
         if in_dev.type != "cuda":
             return flux.to(in_dev)
         return flux
+
+    def _forward_radiance(self, cfg, inp, flux, status, stream, bc, dev, keep, nwave, ncol):
+        import ctypes
+        ds = self.options.ds()
+        f64 = torch.float64
+        phi0 = None
+        if bc.get("phi0") is not None:
+            phi0 = torch.as_tensor(bc["phi0"], dtype=f64).expand((nwave, ncol)).to(dev)
+            phi0 = phi0.contiguous()
+            keep.append(phi0)
+        arr = lambda xs: (ctypes.c_double * max(1, len(xs)))(*xs)  # noqa: E731
+        ut, mu, ph = arr(ds.utau), arr(self._umu), arr(self._phi)
+        rad = _lib.HdRadiance(ntau=len(ds.utau) if self.usrtau else 0,
+                              utau=ctypes.cast(ut, ctypes.c_void_p),
+                              numu=len(self._umu), umu=ctypes.cast(mu, ctypes.c_void_p),
+                              nphi=len(self._phi), phi=ctypes.cast(ph, ctypes.c_void_p),
+                              phi0=phi0.data_ptr() if phi0 is not None else None,
+                              onlyfl=int(self.onlyfl))
+        uu = None
+        if not self.onlyfl:
+            uu = torch.empty((nwave, ncol, len(self._phi), ds.ntau, len(self._umu)), dtype=f64,
+                             device=dev)
+        with torch.cuda.device(dev):
+            _context(dev.index).solve_radiance(
+                cfg, inp, rad, flux.data_ptr(), uu.data_ptr() if uu is not None else None,
+                status.data_ptr() if status is not None else None, stream.cuda_stream)
+        self._rad = uu
+
+
+def _lib_loaded() -> bool:
+    try:
+        _lib.load()
+        return True
+    except OSError:
+        return False
+
+
+def _gauss(nstr):
+    import numpy as np
+    x, w = np.polynomial.legendre.leggauss(nstr // 2)
+    return list(0.5 * (x + 1.0)), list(0.5 * w)
