@@ -15,6 +15,12 @@
 //     harp_amd::Disort disort(op);
 //     auto flux = disort->forward(prop, &bc);          // (nwave, ncol, nlyr+1, 2)
 //
+// Without `onlyfl` the module also computes radiances (hd_solve_radiance; the
+// configuration of tests/test_disort.cpp:13-55): at user_mu x user_phi with
+// `usrang` (else the quadrature cosines), at user_tau with `usrtau` (else the
+// levels); `disort->get_rad()` returns (nwave, ncol, nphi, ntau, numu).  With
+// `usrtau` the fluxes are at the user depths, index 0 = the deepest.
+//
 // Tensors may live on the CPU (staged through the GPU, result returned on the
 // CPU) or on a ROCm device (zero-copy, torch's current stream).  Errors are
 // raised with TORCH_CHECK, like the reference (radiation_band.cpp:25,50,71).
@@ -26,6 +32,7 @@
 #include <torch/nn/modules/container/any.h>
 #include <torch/torch.h>
 
+#include <cmath>
 #include <map>
 #include <memory>
 #include <set>
@@ -59,7 +66,35 @@ constexpr int IDN = 1;  // downward flux (rfldir + rfldn)
 
 struct DisortState {  // subset of cdisort's disort_state reachable via ds()
   int nlyr = 1, nstr = 4, nmom = 4, nphi = 0, ntau = 0, numu = 0;
+  std::vector<double> utau;  // user optical depths (usrtau), filled by reset()
 };
+
+// pydisort's scattering_moments(nmom, PhaseMomentOptions) for the phase
+// functions with closed-form moments (used at tests/test_disort.cpp:44-47):
+// chi_1..chi_nmom of the isotropic, Rayleigh and Henyey-Greenstein functions
+enum PhaseFunctionType { kIsotropic, kRayleigh, kHenyeyGreenstein };
+struct PhaseMomentOptions {
+  PhaseMomentOptions() = default;
+  PhaseMomentOptions& type(PhaseFunctionType t) {
+    type_ = t;
+    return *this;
+  }
+  PhaseMomentOptions& gg(double g) {
+    gg_ = g;
+    return *this;
+  }
+  PhaseFunctionType type_ = kIsotropic;
+  double gg_ = 0.0;
+};
+inline torch::Tensor scattering_moments(int nmom, PhaseMomentOptions const& op) {
+  auto m = torch::zeros({nmom}, torch::kFloat64);
+  auto a = m.accessor<double, 1>();
+  for (int l = 1; l <= nmom; ++l) {
+    if (op.type_ == kRayleigh) a[l - 1] = l == 2 ? 0.1 : 0.0;
+    if (op.type_ == kHenyeyGreenstein) a[l - 1] = std::pow(op.gg_, l);
+  }
+  return m;
+}
 
 struct DisortOptions {
   DisortOptions() = default;
@@ -116,9 +151,52 @@ class DisortImpl : public torch::nn::Cloneable<DisortImpl> {
       TORCH_CHECK((int)options.wave_lower().size() == options.nwave() &&
                       (int)options.wave_upper().size() == options.nwave(),
                   "Disort: planck needs wave_lower/wave_upper of size nwave");
+    onlyfl_ = flags.count("onlyfl") > 0;
+    usrtau_ = flags.count("usrtau") > 0;
+    radiance_ = !onlyfl_ || usrtau_;
+    rad_ = torch::Tensor();
+    auto& d = options.ds();
+    if (radiance_) {
+      TORCH_CHECK(d.nstr <= 16, "Disort: radiances / user depths need nstr <= 16");
+      if (usrtau_) {
+        d.utau = options.user_tau();
+        TORCH_CHECK(!d.utau.empty(), "Disort: usrtau set but user_tau is empty");
+        for (size_t i = 0; i < d.utau.size(); ++i)
+          TORCH_CHECK(d.utau[i] >= 0 && (i == 0 || d.utau[i] >= d.utau[i - 1]),
+                      "Disort: user_tau must be >= 0 and ascending");
+        d.ntau = (int)d.utau.size();
+      } else {
+        d.utau.clear();
+        d.ntau = d.nlyr + 1;
+      }
+      if (flags.count("usrang")) {
+        umu_ = options.user_mu();
+        TORCH_CHECK(!umu_.empty(), "Disort: usrang needs user_mu");
+        for (double x : umu_)
+          TORCH_CHECK(x != 0.0 && std::fabs(x) <= 1.0, "Disort: user_mu must be in [-1,0)U(0,1]");
+      } else {
+        std::vector<double> mu(d.nstr / 2), w(d.nstr / 2);
+        TORCH_CHECK(hd_quadrature(d.nstr, mu.data(), w.data()) == HD_OK, "Disort: quadrature");
+        umu_.clear();
+        for (int i = d.nstr / 2 - 1; i >= 0; --i) umu_.push_back(-mu[i]);
+        for (double x : mu) umu_.push_back(x);
+      }
+      phi_ = options.user_phi();
+      if (phi_.empty()) phi_ = {0.0};
+      d.numu = onlyfl_ ? 0 : (int)umu_.size();
+      d.nphi = onlyfl_ ? 0 : (int)phi_.size();
+    }
   }
 
   DisortState& ds() { return options.ds(); }
+
+  //! radiances of the last forward: (nwave, ncol, nphi, ntau, numu)
+  torch::Tensor get_rad(torch::TensorOptions const& op = {}) const {
+    TORCH_CHECK(!onlyfl_, "Disort.get_rad: radiances are off (onlyfl flag)");
+    TORCH_CHECK(rad_.defined(), "Disort.get_rad: call forward first");
+    return rad_.to(op.has_device() ? op.device() : rad_.device(),
+                   op.has_dtype() ? op.dtype() : rad_.dtype());
+  }
 
   //! flux (nwave, ncol, nlyr+1, 2); level 0 = surface; [..,0] up, [..,1] down
   torch::Tensor forward(torch::Tensor prop, std::map<std::string, torch::Tensor>* bc,
@@ -142,7 +220,6 @@ class DisortImpl : public torch::nn::Cloneable<DisortImpl> {
         bool ok = k == "phi0";
         for (auto key : keys) ok = ok || k == key;
         TORCH_CHECK(ok, "Disort.forward: unknown boundary condition '", k, "'");
-        if (k == "phi0") continue;
         auto t = to_dev(v.expand({nwave, ncol}));
         b[k] = t;
       }
@@ -155,7 +232,8 @@ class DisortImpl : public torch::nn::Cloneable<DisortImpl> {
       wl = torch::tensor(options.wave_lower(), f64);
       wu = torch::tensor(options.wave_upper(), f64);
     }
-    auto flux = torch::empty({nwave, ncol, nlyr + 1, 2}, f64);
+    const int nlev = radiance_ ? options.ds().ntau : nlyr + 1;
+    auto flux = torch::empty({nwave, ncol, nlev, 2}, f64);
 
     auto ptr = [](const torch::Tensor& t) -> const double* {
       return t.defined() ? t.data_ptr<double>() : nullptr;
@@ -170,14 +248,30 @@ class DisortImpl : public torch::nn::Cloneable<DisortImpl> {
                  bp("albedo"), bp("btemp"), bp("ttemp"),  bp("temis"), bp("fisot"),
                  ptr(tf),     ptr(wl),     ptr(wu)};
     auto stream = at::hip::getCurrentHIPStream(dev.index()).stream();
-    int rc = hd_solve(context(dev.index()), &cfg, &in, flux.data_ptr<double>(), nullptr,
-                      reinterpret_cast<void*>(stream));
+    int rc;
+    if (radiance_) {
+      auto const& d = options.ds();
+      hd_radiance rad{usrtau_ ? d.ntau : 0, d.utau.data(), (int)umu_.size(), umu_.data(),
+                      (int)phi_.size(), phi_.data(), bp("phi0"), onlyfl_ ? 1 : 0};
+      torch::Tensor uu;
+      if (!onlyfl_) uu = torch::empty({nwave, ncol, (int)phi_.size(), d.ntau, (int)umu_.size()}, f64);
+      rc = hd_solve_radiance(context(dev.index()), &cfg, &in, &rad, flux.data_ptr<double>(),
+                             uu.defined() ? uu.data_ptr<double>() : nullptr, nullptr,
+                             reinterpret_cast<void*>(stream));
+      rad_ = uu.defined() ? (in_dev.is_cuda() ? uu : uu.to(in_dev)) : uu;
+    } else {
+      rc = hd_solve(context(dev.index()), &cfg, &in, flux.data_ptr<double>(), nullptr,
+                    reinterpret_cast<void*>(stream));
+    }
     TORCH_CHECK(rc == HD_OK, "DisortWrapper::Run failed: ", hd_last_error(context(dev.index())));
     return in_dev.is_cuda() ? flux : flux.to(in_dev);
   }
 
  private:
   bool planck_ = false;
+  bool onlyfl_ = true, usrtau_ = false, radiance_ = false;
+  std::vector<double> umu_, phi_;
+  torch::Tensor rad_;
 
   static hd_context* context(int device) {
     static std::map<int, std::unique_ptr<hd_context, int (*)(hd_context*)>> ctxs;

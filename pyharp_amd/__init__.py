@@ -10,6 +10,8 @@ from .index import IDN, IEX, IPM, ISS, IUP  # noqa: F401
 from .rtsolver import RTSolver  # noqa: F401
 from .disort import Disort, DisortOptions  # noqa: F401
 from .layer2level import Layer2LevelOptions, layer2level  # noqa: F401
+from .scattering import PhaseMomentOptions, scattering_moments  # noqa: F401
 
 __all__ = ["Disort", "DisortOptions", "RTSolver", "layer2level", "Layer2LevelOptions",
-           "IEX", "ISS", "IPM", "IUP", "IDN"]
+           "IEX", "ISS", "IPM", "IUP", "IDN", "PhaseMomentOptions",
+           "scattering_moments"]

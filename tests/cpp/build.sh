@@ -1,6 +1,7 @@
 #!/bin/bash
 # Compile the C++ drop-in checks against the container's libtorch (ROCm build)
-# and the in-tree libhdisort.so.  Outputs: tests/cpp/disort_dropin, tests/cpp/amars_sw_dropin
+# and the in-tree libhdisort.so.  Outputs: tests/cpp/disort_dropin, tests/cpp/amars_sw_dropin,
+# tests/cpp/disort_rad_dropin
 set -euo pipefail
 HERE=$(cd "$(dirname "$0")" && pwd)
 ROOT=$(cd "$HERE/../.." && pwd)
@@ -15,4 +16,5 @@ build() {
 }
 build disort_dropin &
 build amars_sw_dropin &
-wait %1 && wait %2
+build disort_rad_dropin &
+wait %1 && wait %2 && wait %3

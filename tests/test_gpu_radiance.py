@@ -199,3 +199,28 @@ def test_radiance_argument_errors():
         _disort(8, 2, 1, 1, flags="usrang,lamber", umu=[0.0], phi=[0.0])
     with pytest.raises(RuntimeError):
         _disort(8, 2, 1, 1, flags="usrtau,onlyfl,lamber", utau=[0.5, 0.1])
+
+
+def test_cpp_disort_rad():
+    """tests/cpp/disort_rad_dropin.cpp: the reference's tests/test_disort.cpp
+    main() against harp_amd::Disort (include/harp_amd/disort.hpp)."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "tests", "cpp", "disort_rad_dropin")
+    if not os.path.exists(exe):
+        subprocess.run([os.path.join(root, "tests", "cpp", "build.sh")], check=True)
+    out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout.split("\n")
+    c = disotest()["cases"]["1a"]
+    rad = {(int(l.split()[1]), int(l.split()[2])): float(l.split()[3])
+           for l in out if l.startswith("rad")}
+    exp = np.asarray(c["uu"])
+    for (lu, iu), v in rad.items():
+        assert abs(v - exp[lu, iu]) <= 5e-6 * abs(exp[lu, iu]) + 1e-6, (lu, iu, v)
+    assert len(rad) == 12
+    flux = {int(l.split()[1]): (float(l.split()[2]), float(l.split()[3]))
+            for l in out if l.startswith("flux")}
+    # index 0 = the deepest user depth (tau = 0.03125)
+    assert abs(flux[1][0] - c["flup"][0]) <= 5e-6 * c["flup"][0]
+    dn_bot = c["rfldir"][1] + c["rfldn"][1]
+    assert abs(flux[0][1] - dn_bot) <= 5e-6 * dn_bot

@@ -151,3 +151,13 @@ def test_product_never_imports_oracle():
                     src = f.read()
                 assert not re.search(r"^\s*(from|import)\s+oracle", src, re.M), fn
                 assert "hdoracle" not in src, fn
+
+
+def test_scattering_moments():
+    from pyharp_amd import PhaseMomentOptions, scattering_moments
+    from pyharp_amd.scattering import kHenyeyGreenstein, kIsotropic, kRayleigh
+    assert scattering_moments(16, PhaseMomentOptions().type(kIsotropic)).abs().sum() == 0
+    r = scattering_moments(8, PhaseMomentOptions().type(kRayleigh))
+    assert r[1] == 0.1 and r.abs().sum() == 0.1
+    h = scattering_moments(4, PhaseMomentOptions().type(kHenyeyGreenstein).gg(0.5))
+    assert torch.allclose(h, torch.tensor([0.5, 0.25, 0.125, 0.0625], dtype=torch.float64))
