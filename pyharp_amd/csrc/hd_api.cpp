@@ -599,7 +599,8 @@ int hd_solve_radiance(hd_context* ctx, const hd_config* cfg, const hd_inputs* in
   const size_t per_unit = hd::rad_scratch_doubles_per_unit(nn, nlyr) + (size_t)ntau * numu;
   const size_t per_solve = (size_t)nm_mode * per_unit + (size_t)(nlyr + 1) + nlyr +
                            (planck ? (size_t)nlyr + 3 : 0);
-  const double budget = 4.0 * 1024.0 * 1024.0 * 1024.0 / 8.0;  // doubles
+  // 16 GB of the 288 GB: chunks of ~1e5 units keep every SIMD busy in the per-unit sweep
+  const double budget = 16.0 * 1024.0 * 1024.0 * 1024.0 / 8.0;  // doubles
   long chunk = std::max<long>(1, std::min<long>(nsolve, (long)(budget / (double)per_solve)));
   chunk = std::min<long>(chunk, 0x7fffffffL / std::max(1, nm_mode));
   if (ctx->chunk > 0) chunk = std::min(chunk, ctx->chunk);

@@ -132,6 +132,28 @@ __device__ __forceinline__ double seg_exp(double a, double c, double t1, double 
   return a * (p1 - p2) / den;
 }
 
+// (pa - pb)/den where pb = pa e^{-y}, y = den * len: the direct quotient, or
+// pa * len * (1 - e^-y)/y by its Taylor series when |y| < 1/2 (den -> 0)
+__device__ __forceinline__ double dexp(double pa, double pb, double den, double len) {
+  const double y = den * len;
+  // sum_{n<=13} (-y)^n/(n+1)!: |y|^14/15! < 5e-17 for |y| < 1/2
+  double ph = 1.0 / 87178291200.0;  // 1/14!
+  ph = fma(ph, -y, 1.0 / 6227020800.0);
+  ph = fma(ph, -y, 1.0 / 479001600.0);
+  ph = fma(ph, -y, 1.0 / 39916800.0);
+  ph = fma(ph, -y, 1.0 / 3628800.0);
+  ph = fma(ph, -y, 1.0 / 362880.0);
+  ph = fma(ph, -y, 1.0 / 40320.0);
+  ph = fma(ph, -y, 1.0 / 5040.0);
+  ph = fma(ph, -y, 1.0 / 720.0);
+  ph = fma(ph, -y, 1.0 / 120.0);
+  ph = fma(ph, -y, 1.0 / 24.0);
+  ph = fma(ph, -y, 1.0 / 6.0);
+  ph = fma(ph, -y, 0.5);
+  ph = fma(ph, -y, 1.0);
+  return fabs(y) < 0.5 ? pa * len * ph : (pa - pb) / den;
+}
+
 // user depth lu of solve sl: the caller's utau or the level depths
 __device__ __forceinline__ double user_tau(const RadArgs& A, int lu, int sl) {
   return A.utau ? A.utau[lu] : A.taus[(size_t)lu * A.ns + sl];
@@ -266,7 +288,8 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
 
   double* rr = A.rrd + (size_t)lc * rad_rec_doubles(NN) * nu + u;
   constexpr int oV = nsym, oK = nsym + NN * NN, oZp = oK + NN, oZm = oZp + NN, oH = oZm + NN;
-  constexpr int oBt = oH + NN, oSl = oBt + 1, oTp = oSl + 1, oOm = oTp + 1;
+  constexpr int oBt = oH + NN, oSl = oBt + 1, oTp = oSl + 1, oOm = oTp + 1, oEk = oOm + 1;
+  constexpr int oE0 = oEk + NN;
 
   double y2[NN], lxd[NN];
   const double fb2 = fb * ((m == 0 ? 0.5 : 1.0) / kPi);
@@ -441,7 +464,9 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
     const double delta = x > 1.0e-8 ? th * rcp_nr(kk[j] > 0.0 ? kk[j] : 1.0) : 0.5 * taup;
     dsq[j] = sqrt(delta);
     gsq[j] = sqrt(kk[j] * th);
+    rr[(oEk + j) * nu] = 1.0 - mm;  // exp(-k tau') for the user-angle kernel
   }
+  rr[oE0 * nu] = e0;
 #pragma unroll
   for (int j = 0; j < NN; ++j) {
     double x[NN];
@@ -996,13 +1021,17 @@ __global__ __launch_bounds__(64) void hd_rad_user_kernel(RadArgs A) {
   constexpr int N = 2 * NN;
   constexpr int nsym = NN * (NN + 1) / 2;
   constexpr int oZp = nsym + NN * NN + NN, oZm = oZp + NN, oH = oZm + NN, oBt = oH + NN;
+  constexpr int oEk = oBt + 4, oE0 = oEk + NN;
   const Quad<NN>& Qc = quad_r<NN>();
+  // grid.y = mode (uniform per block: the mode-m tables are scalar loads);
+  // user angle fastest inside a block: the lanes of one unit read the same
+  // layer records (one cache segment per unit instead of one per angle)
   const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= (long)A.nu * A.numu) return;
-  const int iu = (int)(id / A.nu);
-  const int u = (int)(id - (long)iu * A.nu);
-  const int m = u / A.ns;
-  const int sl = u - m * A.ns;
+  if (id >= (long)A.ns * A.numu) return;
+  const int sl = (int)(id / A.numu);
+  const int iu = (int)(id - (long)sl * A.numu);
+  const int m = blockIdx.y;
+  const int u = m * A.ns + sl;
   const long s = A.s0 + sl;
   const int L = A.nlyr, np = A.nprop, nm = A.nmom;
   const size_t nu = A.nu;
@@ -1061,50 +1090,74 @@ __global__ __launch_bounds__(64) void hd_rad_user_kernel(RadArgs A) {
     const double rf = om / (1.0 - f);
     double cue[NN], cuo[NN];
     double x0 = 0.0;
-#pragma unroll
-    for (int i = 0; i < NN; ++i) cue[i] = cuo[i] = 0.0;
+    double gy[N];
 #pragma unroll
     for (int l = 0; l < N; ++l) {
       const double chi = l == 0 ? 1.0 : (l <= nm ? q[1 + l] : 0.0);
       const double gl = (2 * l + 1) * (chi - f) * rf;
-      const double t = 0.5 * gl * yu[l];
+      gy[l] = 0.5 * gl * yu[l];
       x0 = fma(gl * yu[l], y0[l], x0);
-      const bool ev = ((l + m) & 1) == 0;
-      const double te = ev ? t : 0.0, to = ev ? 0.0 : t;
+    }
+    // even/odd parts in l + m: m is uniform per block, so is the branch
+    auto lsum = [&](int par) {
 #pragma unroll
       for (int i = 0; i < NN; ++i) {
-        const double p = lam[l * NN + i];
-        cue[i] = fma(te, p, cue[i]);
-        cuo[i] = fma(to, p, cuo[i]);
+        double e = 0.0, o = 0.0;
+#pragma unroll
+        for (int l2 = 0; l2 < NN; ++l2) {
+          e = fma(gy[2 * l2 + par], lam[(2 * l2 + par) * NN + i], e);
+          o = fma(gy[2 * l2 + 1 - par], lam[(2 * l2 + 1 - par) * NN + i], o);
+        }
+        cue[i] = e;
+        cuo[i] = o;
       }
-    }
-    double lch[NN][NN], rd[NN], v[NN][NN], kk[NN];
-    load_layer<NN>(A, lc, u, lch, rd, v, kk);
+    };
+    if (m & 1) lsum(1);
+    else lsum(0);
     const double* rr = A.rrd + (size_t)lc * rad_rec_doubles(NN) * nu + u;
     const double bt = rr[oBt * nu], slope = rr[(oBt + 1) * nu], taup = rr[(oBt + 2) * nu];
-    // ce = V^T L^T (sd cue), co = -k V^T L^-1 (sd cuo)
+    // ce = V^T L^T (sd cue), co = -k V^T L^-1 (sd cuo); L and V streamed from the
+    // record (each element used once), not held in registers
     double a1[NN], b1[NN];
 #pragma unroll
-    for (int i = 0; i < NN; ++i) b1[i] = Qc.sd[i] * cuo[i];
-    lower_solve<NN>(lch, rd, b1);
-#pragma unroll
     for (int i = 0; i < NN; ++i) {
-      double a = 0.0;
+      a1[i] = 0.0;
+      b1[i] = Qc.sd[i] * cuo[i];
+    }
 #pragma unroll
-      for (int kx = i; kx < NN; ++kx) a = fma(lch[kx][i], Qc.sd[kx] * cue[kx], a);
-      a1[i] = a;
+    for (int i = 0; i < NN; ++i) {  // row i of L: a1 += L[i][:]^T (sd cue)_i ; b1 forward subst.
+      const double* li = rr + (size_t)(i * (i + 1) / 2) * nu;
+      const double ce_i = Qc.sd[i] * cue[i];
+      double t = b1[i];
+#pragma unroll
+      for (int k2 = 0; k2 < i; ++k2) {
+        const double l = li[k2 * nu];
+        a1[k2] = fma(l, ce_i, a1[k2]);
+        t = fma(-l, b1[k2], t);
+      }
+      const double d = li[i * nu];
+      a1[i] = fma(d, ce_i, a1[i]);
+      b1[i] = t / d;
     }
     const double* co = A.cst + (size_t)lc * 2 * NN * nu + u;
-    double hpl[NN], hmi[NN];
+    const double* vr = rr + (size_t)nsym * nu;
+    double kk[NN], hpl[NN], hmi[NN];
 #pragma unroll
     for (int j = 0; j < NN; ++j) {
-      double ce = 0.0, cx = 0.0;
+      hpl[j] = hmi[j] = 0.0;
+      kk[j] = rr[(nsym + NN * NN + j) * nu];
+    }
 #pragma unroll
-      for (int i = 0; i < NN; ++i) {
-        ce = fma(v[i][j], a1[i], ce);
-        cx = fma(v[i][j], b1[i], cx);
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int j = 0; j < NN; ++j) {
+        const double vij = vr[(i * NN + j) * nu];
+        hpl[j] = fma(vij, a1[i], hpl[j]);  // ce
+        hmi[j] = fma(vij, b1[i], hmi[j]);  // V^T b1
       }
-      cx *= -kk[j];
+#pragma unroll
+    for (int j = 0; j < NN; ++j) {
+      const double ce = hpl[j], cx = -kk[j] * hmi[j];
       hpl[j] = co[j * nu] * (ce + cx);
       hmi[j] = co[(NN + j) * nu] * (ce - cx);
     }
@@ -1129,6 +1182,7 @@ __global__ __launch_bounds__(64) void hd_rad_user_kernel(RadArgs A) {
       a1t = slope * ce0;
       a0 = fma(bt, ce0, 2.0 * slope * wo);
     }
+    // general segment [t1 (evaluation), t2 (far end)] for user depths inside the layer
     auto integ = [&](double t1, double t2) {
       double r = 0.0;
 #pragma unroll
@@ -1143,28 +1197,59 @@ __global__ __launch_bounds__(64) void hd_rad_user_kernel(RadArgs A) {
       }
       return r;
     };
+    // whole layer, entry -> exit, from the stored exp(-k tau'), exp(-tau'/mu0)
+    // and one exp(-tau'/|mu|): the +k terms decay along upward rays, the -k
+    // terms along downward ones; the other family meets 1 - k|mu| -> 0 and goes
+    // through dexp's (1 - e^-y)/y series
+    const double anu = fabs(muu);
+    const double lmu = taup / anu;
+    const double emu = exp(-lmu);
+    double lay = 0.0;
+#pragma unroll
+    for (int j = 0; j < NN; ++j) {
+      const double ek = rr[(oEk + j) * nu];
+      const double reg = (1.0 - ek * emu) / fma(kk[j], anu, 1.0);
+      const double sng = dexp(ek, emu, fma(-kk[j], anu, 1.0), lmu);
+      lay = up ? fma(hpl[j], reg, fma(hmi[j], sng, lay)) : fma(hpl[j], sng, fma(hmi[j], reg, lay));
+    }
+    if (beam) {
+      const double e0l = rr[oE0 * nu];
+      lay += up ? ab * (1.0 - e0l * emu) / fma(anu, rmu0, 1.0)
+                : ab * dexp(e0l, emu, fma(-anu, rmu0, 1.0), lmu);
+    }
+    if (therm) {  // (a0 + a1 t1 + a1 mu) - (a0 + a1 t2 + a1 mu) e^{-(t2-t1)/mu}
+      lay += up ? (a0 + a1t * muu) - (a0 + a1t * taup + a1t * muu) * emu
+                : (a0 + a1t * taup + a1t * muu) - (a0 + a1t * muu) * emu;
+    }
+    const double cin = cur;                // at the entry boundary
+    const double cout = fma(cin, emu, lay);  // at the exit boundary
     const double tau = tbot - ttop;
     const double scale = tau > 0.0 ? taup / tau : 0.0;
-    const double tfar = up ? taup : 0.0;
+    // value at local depth t: boundaries from cin/cout, interior by integ
+    auto at = [&](double t) {
+      const double tin = up ? taup : 0.0;  // entry depth
+      if (t == tin) return cin;
+      if (t == taup - tin) return cout;
+      return cin * exp(-fabs(tin - t) / anu) + integ(t, tin);
+    };
     if (up) {
       while (k >= 0 && user_tau(A, k, sl) >= ttop) {
         const double t = fmin(fmax((user_tau(A, k, sl) - ttop) * scale, 0.0), taup);
-        const double val = cur * exp(-(tfar - t) / muu) + integ(t, tfar);
+        const double val = at(t);
         A.radm[((size_t)k * A.numu + iu) * nu + u] = val;
         chk += val;
         --k;
       }
-      cur = cur * exp(-taup / muu) + integ(0.0, taup);
     } else {
       while (k < A.ntau && user_tau(A, k, sl) <= tbot) {
         const double t = fmin(fmax((user_tau(A, k, sl) - ttop) * scale, 0.0), taup);
-        const double val = cur * exp(t / muu) + integ(t, 0.0);
+        const double val = at(t);
         A.radm[((size_t)k * A.numu + iu) * nu + u] = val;
         chk += val;
         ++k;
       }
-      cur = cur * exp(taup / muu) + integ(taup, 0.0);
     }
+    cur = cout;
   }
   // user depths beyond the bottom (flagged by the taus kernel): bottom value
   for (; k < A.ntau && !up; ++k) A.radm[((size_t)k * A.numu + iu) * nu + u] = cur;
@@ -1271,9 +1356,9 @@ static void launch_rad(const RadArgs& a, bool radiances, hipStream_t st) {
   hipLaunchKernelGGL(hd_rad_flux_kernel<NN>, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, st,
                      a);
   if (radiances && a.numu > 0 && a.nphi > 0) {
-    const long nr = (long)a.nu * a.numu;
-    hipLaunchKernelGGL(hd_rad_user_kernel<NN>, dim3((unsigned)((nr + 63) / 64)), dim3(64), 0, st,
-                       a);
+    const long nr = (long)a.ns * a.numu;
+    hipLaunchKernelGGL(hd_rad_user_kernel<NN>, dim3((unsigned)((nr + 63) / 64), (unsigned)a.nm),
+                       dim3(64), 0, st, a);
     const long na = (long)a.ns * a.nphi * a.ntau * a.numu;
     hipLaunchKernelGGL(hd_rad_azimuth_kernel, dim3((unsigned)((na + 255) / 256)), dim3(256), 0,
                        st, a);

@@ -15,9 +15,10 @@ template <int NN>
 __host__ __device__ constexpr int rad_nsym() {
   return NN * (NN + 1) / 2;
 }
-// per-(unit, layer) radiance record: L (packed lower), V, k, Z+, Z-, h, B_top, dB/dtau', tau', omega'
+// per-(unit, layer) radiance record: L (packed lower), V, k, Z+, Z-, h, B_top,
+// dB/dtau', tau', omega', exp(-k tau'), exp(-tau'/mu0)
 __host__ __device__ constexpr int rad_rec_doubles(int nn) {
-  return nn * (nn + 1) / 2 + nn * nn + 4 * nn + 4;
+  return nn * (nn + 1) / 2 + nn * nn + 5 * nn + 5;
 }
 // per-(unit, layer) sweep record for the back-substitution: ZT, t, R_above (packed), S_down
 __host__ __device__ constexpr int rad_bsub_doubles(int nn) {
