@@ -1,6 +1,12 @@
 """amars LW correlated-k case on the device, as pyharp's examples/amars_lw.cpp.
 
-    python examples/amars_lw.py [--nstr 8] [--ngpoint 16] [--nlyr 40]
+    python examples/amars_lw.py [--nstr 8] [--ngpoint 16] [--nlyr 40] [--table FILE.nc]
+
+With ``--table`` (an RFM ck file in classic netCDF, e.g. amarsw-ck-B1.nc
+converted with ``nccopy -k classic``) this is amars_lw.cpp:40-88 step for
+step: RFM CO2 and H2O attenuators on the device (pyharp_amd.opacity.RFM),
+prop = prop1 + prop2, the Planck solve and the band flux with the file's ck
+weights (read_weights_rfm).  Without it:
 
 The reference reads CO2/H2O k-distributions from amarsw-ck-B1.nc through RFM
 (amars_lw.cpp:41-60); that file is git-ignored upstream and netCDF is not in
@@ -25,6 +31,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 from pyharp_amd import Disort, DisortOptions, layer2level  # noqa: E402
+from pyharp_amd.opacity import RFM, AttenuatorOptions, read_weights_rfm  # noqa: E402
 from pyharp_amd.spectral import band_flux  # noqa: E402
 
 
@@ -49,13 +56,40 @@ def run(nstr=8, ngpoint=16, nlyr=40, ncol=1, device=0, seed=20250217):
     return {"prop": prop, "flux": flux, "temf": temf, "bflux": band_flux(flux, weights)}
 
 
+def run_rfm(table, nstr=8, nlyr=40, ncol=1, device=0):
+    """amars_lw.cpp:40-88 with the RFM tables of `table`"""
+    dev = torch.device("cuda", device)
+    op = AttenuatorOptions().species_names(["CO2", "H2O"]).species_weights([44.0e-3, 18.0e-3])
+    co2 = RFM(op.copy().species_ids([0]).opacity_files([table]))
+    h2o = RFM(op.copy().species_ids([1]).opacity_files([table]))
+    nwave = co2.kdata.shape[0]
+    conc = torch.ones((ncol, nlyr, 2), dtype=torch.float64, device=dev)
+    kwargs = {"pres": torch.full((ncol, nlyr), 10.e5, dtype=torch.float64, device=dev),
+              "temp": torch.full((ncol, nlyr), 300.0, dtype=torch.float64, device=dev)}
+    prop = co2.forward(conc, kwargs) + h2o.forward(conc, kwargs)
+    dop = DisortOptions().header("running amars lw").flags(
+        "lamber,quiet,onlyfl,planck,intensity_correction,old_intensity_correction,"
+        "print-input,print-phase-function,print-fluxes")
+    dop.nwave(nwave).ncol(ncol).device(device)
+    dop.wave_lower([1.0] * nwave).wave_upper([150.0] * nwave)
+    dop.ds().nlyr, dop.ds().nstr, dop.ds().nmom = nlyr, nstr, nstr
+    bc = {"albedo": torch.ones((nwave, ncol), dtype=torch.float64, device=dev),
+          "btemp": torch.full((nwave, ncol), 300.0, dtype=torch.float64, device=dev)}
+    temf = layer2level(kwargs["temp"])
+    flux = Disort(dop).forward(prop, bc, temf)
+    weights = read_weights_rfm(table).to(dev)
+    return {"prop": prop, "flux": flux, "temf": temf, "weights": weights,
+            "bflux": band_flux(flux, weights)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nstr", type=int, default=8)
     ap.add_argument("--ngpoint", type=int, default=16)
     ap.add_argument("--nlyr", type=int, default=40)
+    ap.add_argument("--table", default=None)
     a = ap.parse_args()
-    r = run(a.nstr, a.ngpoint, a.nlyr)
+    r = run_rfm(a.table, a.nstr, a.nlyr) if a.table else run(a.nstr, a.ngpoint, a.nlyr)
     print("bflx =", r["bflux"].cpu().numpy())
 
 

@@ -63,6 +63,27 @@ int hd_band_optics(const hd_attenuator *atts, int natt, const double *coord, int
                    int nwave, const double *conc, int ncol, int nlyr, int nspecies,
                    const double *dz, int nprop, double *prop, void *stream);
 
+/* one RFM absorption table (harp::RFMImpl after reset(), src/opacity/rfm.cpp:30-120;
+ * the reference reads it from netCDF: dims Wavenumber/Pressure/TempGrid, variables
+ * of the same names, the reference Temperature profile and one variable per
+ * species).  All arrays are DEVICE pointers. */
+typedef struct hd_rfm_table {
+  int nwave, npres, ntemp;
+  const double *wave;  /* [nwave] wavenumber axis                                */
+  const double *lnp;   /* [npres] ln(pressure [Pa]) axis (the reference's log_)   */
+  const double *tgrid; /* [ntemp] temperature-anomaly axis [K]                     */
+  const double *tref;  /* [npres] reference temperature profile [K]               */
+  const double *kdata; /* [nwave][npres][ntemp] ln(m^2/kmol)                       */
+  int species;         /* index into the last dim of conc                         */
+} hd_rfm_table;
+
+/* harp::RFMImpl::forward (rfm.cpp:122-197): out [nwave][ncol][nlyr] (nprop = 1) =
+ * 1e-3 exp(interpn(kdata; wave_w, ln p, T - T_ref(ln p))) conc[..][species];
+ * pres [Pa], temp [K]: [ncol][nlyr]; conc [ncol][nlyr][nspecies] mol/m^3 */
+int hd_rfm_attenuate(const hd_rfm_table *t, const double *conc, int ncol, int nlyr,
+                     int nspecies, const double *pres, const double *temp, double *out,
+                     void *stream);
+
 /* bflux [ncol][nlev][2] = sum_w weight[w] flux[w][ncol][nlev][2] (fixed order) */
 int hd_band_flux(const double *flux, const double *weight, int nwave, int ncol, int nlev,
                  double *bflux, void *stream);

@@ -204,3 +204,52 @@ def amars_sw_atmosphere(profile_path, nlyr=40, g=3.711, mean_mol_weight=0.044, R
         new_rho[k] = (new_p[k] * mean_mol_weight) / (R * new_T[k])
     dz = calc_dz(nlyr, new_p, new_rho, g)
     return conc, new_rho, dz, new_p
+
+
+def interpn(coor, data, axes):
+    """src/math/interpn.h:34-76 for any ndim (nval = 1): data has shape
+    tuple(len(a) for a in axes); the recursion and arithmetic order of the
+    reference (lerp of the two sub-interpolations along the leading axis)."""
+    axis = axes[0]
+    n = len(axis)
+    x = coor[0]
+    i1 = locate(axis, x)
+    if i1 == -1:
+        i1 = i2 = 0
+    elif i1 == n - 1:
+        i2 = n - 1
+    else:
+        i2 = i1 + 1
+    if len(axes) == 1:
+        v1, v2 = data[i1], data[i2]
+    else:
+        v1 = interpn(coor[1:], data[i1], axes[1:])
+        v2 = interpn(coor[1:], data[i2], axes[1:])
+    x1, x2 = axis[i1], axis[i2]
+    if x2 != x1:
+        return ((x - x1) * v2 + (x2 - x) * v1) / (x2 - x1)
+    return (v1 + v2) / 2.0
+
+
+def rfm_forward(wave, lnp_axis, temp_axis, ref_temp, kdata, conc, pres, temp, species):
+    """harp::RFMImpl::forward (src/opacity/rfm.cpp:122-197) + get_reftemp
+    (:199-225): tempa = T - interp1(ln p; ln p_ref, T_ref); k = interpn over
+    (wave, ln p, tempa) of ln(m^2/kmol); prop = 1e-3 exp(k) conc[..., species].
+    Returns (nwave, ncol, nlyr, 1)."""
+    conc = np.asarray(conc, np.float64)
+    ncol, nlyr = conc.shape[:2]
+    nwave = len(wave)
+    out = np.zeros((nwave, ncol, nlyr, 1))
+    lnp = np.log(np.asarray(pres, np.float64))
+    tref = np.zeros((ncol, nlyr))
+    for c in range(ncol):
+        for l in range(nlyr):
+            tref[c, l] = interpn([lnp[c, l]], np.asarray(ref_temp), [lnp_axis])
+    tempa = np.asarray(temp, np.float64) - tref
+    for w in range(nwave):
+        for c in range(ncol):
+            for l in range(nlyr):
+                v = interpn([wave[w], lnp[c, l], tempa[c, l]], kdata,
+                            [wave, lnp_axis, temp_axis])
+                out[w, c, l, 0] = 1.0e-3 * np.exp(v) * conc[c, l, species]
+    return out

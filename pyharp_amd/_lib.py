@@ -28,8 +28,8 @@ EXPORTED = ("hd_version", "hd_last_error", "hd_context_create", "hd_context_dest
             "hd_context_reserve", "hd_solve", "hd_solve_radiance", "hd_quadrature")
 
 # every symbol include/hdharp.h declares (harp-side steps around the solve)
-HARP_EXPORTED = ("hd_attenuate", "hd_band_optics", "hd_band_flux", "hd_heating_rate",
-                 "hd_spherical_flux_correction")
+HARP_EXPORTED = ("hd_attenuate", "hd_band_optics", "hd_rfm_attenuate", "hd_band_flux",
+                 "hd_heating_rate", "hd_spherical_flux_correction")
 HD_COORD_WAVELENGTH, HD_COORD_WAVENUMBER = 0, 1
 
 _dp = ctypes.c_void_p
@@ -37,6 +37,12 @@ _dp = ctypes.c_void_p
 
 class HdAttenuator(ctypes.Structure):
     _fields_ = [("nrow", ctypes.c_int), ("wavelength", _dp), ("kext", _dp), ("ssa", _dp),
+                ("species", ctypes.c_int)]
+
+
+class HdRfmTable(ctypes.Structure):
+    _fields_ = [("nwave", ctypes.c_int), ("npres", ctypes.c_int), ("ntemp", ctypes.c_int),
+                ("wave", _dp), ("lnp", _dp), ("tgrid", _dp), ("tref", _dp), ("kdata", _dp),
                 ("species", ctypes.c_int)]
 
 
@@ -96,6 +102,8 @@ def load(path: str = LIB_PATH):
                                  _dp]
     lib.hd_band_optics.argtypes = [ctypes.POINTER(HdAttenuator), ci, _dp, ci, ci, _dp, ci, ci, ci,
                                    _dp, ci, _dp, _dp]
+    lib.hd_rfm_attenuate.argtypes = [ctypes.POINTER(HdRfmTable), _dp, ci, ci, ci, _dp, _dp, _dp,
+                                     _dp]
     lib.hd_band_flux.argtypes = [_dp, _dp, ci, ci, ci, _dp, _dp]
     lib.hd_heating_rate.argtypes = [_dp, _dp, _dp, cd, ci, ci, _dp, _dp]
     lib.hd_spherical_flux_correction.argtypes = [_dp, _dp, _dp, _dp, ci, ci, _dp]

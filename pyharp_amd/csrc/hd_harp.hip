@@ -212,6 +212,65 @@ int launched(const char* what) {
 }
 
 }  // namespace
+
+// ---- RFM tables (harp::RFMImpl, src/opacity/rfm.cpp:122-225) ----------------
+// interpn.h's index pair and arithmetic on one axis
+__device__ __forceinline__ void bracket(const double* ax, int n, double x, int& i1, int& i2) {
+  i1 = locate_dev(ax, x, n);
+  if (i1 == -1) {
+    i1 = 0;
+    i2 = 0;
+  } else if (i1 == n - 1) {
+    i2 = n - 1;
+  } else {
+    i2 = i1 + 1;
+  }
+}
+__device__ __forceinline__ double lerp_ref(const double* ax, int i1, int i2, double x, double v1,
+                                           double v2) {
+  const double x1 = ax[i1], x2 = ax[i2];
+  return x2 != x1 ? ((x - x1) * v2 + (x2 - x) * v1) / (x2 - x1) : (v1 + v2) / 2.;
+}
+
+// per (col, lyr): ln p and the temperature anomaly T - T_ref(ln p)  [get_reftemp]
+__global__ __launch_bounds__(256) void hd_rfm_state_kernel(hd_rfm_table t, const double* pres,
+                                                           const double* temp, long n,
+                                                           double* work) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double lnp = log(pres[i]);
+  int i1, i2;
+  bracket(t.lnp, t.npres, lnp, i1, i2);
+  const double tref = lerp_ref(t.lnp, i1, i2, lnp, t.tref[i1], t.tref[i2]);
+  work[i] = lnp;
+  work[n + i] = temp[i] - tref;
+}
+
+// per (wave, col, lyr), (col, lyr) fastest: interpn over (wave, ln p, T anomaly)
+// in the reference's nesting, then 1e-3 exp(k) conc
+__global__ __launch_bounds__(256) void hd_rfm_kernel(hd_rfm_table t, const double* conc,
+                                                     int nspecies, long ncl, long n,
+                                                     const double* work, double* out) {
+  const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= n) return;
+  const int w = (int)(id / ncl);
+  const long cl = id - (long)w * ncl;
+  const double xw = t.wave[w], xp = work[cl], xt = work[ncl + cl];
+  int w1, w2, p1, p2, q1, q2;
+  bracket(t.wave, t.nwave, xw, w1, w2);
+  bracket(t.lnp, t.npres, xp, p1, p2);
+  bracket(t.tgrid, t.ntemp, xt, q1, q2);
+  auto at_wave = [&](int iw) {
+    const double* d = t.kdata + (size_t)iw * t.npres * t.ntemp;
+    const double a = lerp_ref(t.tgrid, q1, q2, xt, d[(size_t)p1 * t.ntemp + q1],
+                              d[(size_t)p1 * t.ntemp + q2]);
+    const double b = lerp_ref(t.tgrid, q1, q2, xt, d[(size_t)p2 * t.ntemp + q1],
+                              d[(size_t)p2 * t.ntemp + q2]);
+    return lerp_ref(t.lnp, p1, p2, xp, a, b);
+  };
+  const double v = lerp_ref(t.wave, w1, w2, xw, at_wave(w1), at_wave(w2));
+  out[id] = 1.E-3 * exp(v) * conc[cl * nspecies + t.species];
+}
 }  // namespace hd
 
 using hd::nblk;
@@ -322,6 +381,33 @@ int hd_spherical_flux_correction(double* bflux, const double* x1f, const double*
   hipLaunchKernelGGL(hd::hd_spherical_kernel, dim3(nblk((long)ncol * 2, 64)), dim3(64), 0, s,
                      bflux, x1f, area, vol, ncol, nlev);
   return hd::launched("hd_spherical_flux_correction");
+}
+
+int hd_rfm_attenuate(const hd_rfm_table* t, const double* conc, int ncol, int nlyr, int nspecies,
+                     const double* pres, const double* temp, double* out, void* stream_) {
+  if (!t || ncol < 0 || nlyr < 0 || nspecies < 1 || t->nwave < 1 || t->npres < 1 ||
+      t->ntemp < 1 || t->species < 0 || t->species >= nspecies)
+    return hd::set_global_error(HD_EINVAL, "hd_rfm_attenuate: bad arguments");
+  if (!t->wave || !t->lnp || !t->tgrid || !t->tref || !t->kdata)
+    return hd::set_global_error(HD_EINVAL, "hd_rfm_attenuate: null table array");
+  const long ncl = (long)ncol * nlyr;
+  const long n = ncl * t->nwave;
+  if (n == 0) return HD_OK;
+  if (!conc || !pres || !temp || !out)
+    return hd::set_global_error(HD_EINVAL, "hd_rfm_attenuate: null array");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream_);
+  double* work = nullptr;  // ln p and the temperature anomaly per (col, lyr)
+  if (hipMallocAsync((void**)&work, (size_t)ncl * 2 * sizeof(double), s) != hipSuccess) {
+    (void)hipGetLastError();
+    return hd::set_global_error(HD_ENOMEM, "hd_rfm_attenuate: scratch allocation failed");
+  }
+  hipLaunchKernelGGL(hd::hd_rfm_state_kernel, dim3(nblk(ncl, 256)), dim3(256), 0, s, *t, pres,
+                     temp, ncl, work);
+  hipLaunchKernelGGL(hd::hd_rfm_kernel, dim3(nblk(n, 256)), dim3(256), 0, s, *t, conc, nspecies,
+                     ncl, n, work, out);
+  int rc = hd::launched("hd_rfm_attenuate");
+  (void)hipFreeAsync(work, s);
+  return rc;
 }
 
 }  // extern "C"

@@ -230,3 +230,115 @@ def band_optics(attenuators: Sequence[_TableAttenuator], conc: torch.Tensor, dz:
                                       c.data_ptr(), ncol, nlyr, nsp, d.data_ptr(), nprop,
                                       out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream))
     return out
+
+
+class RFM:
+    """RFM absorption tables (harp::RFMImpl, src/opacity/rfm.hpp, rfm.cpp).
+
+    ``reset()`` reads the table the way rfm.cpp:30-120 does -- dimensions
+    ``Wavenumber``, ``Pressure``, ``TempGrid``; variables of the same names
+    (pressure converted to ln p), the reference ``Temperature`` profile, and
+    the absorption variable named after ``species_names[species_ids[0]]``
+    (nwave, npres, ntemp) in ln(m^2/kmol) -- through the classic-netCDF reader
+    (``pyharp_amd.ncread``; netCDF-4/HDF5 files are refused).  ``from_arrays``
+    builds the same module from in-memory tables.  ``forward(conc, kwargs)``
+    with ``kwargs["pres"]`` [Pa] and ``kwargs["temp"]`` [K] (ncol, nlyr) returns
+    (nwave, ncol, nlyr, 1) = 1e-3 exp(k) conc [1/m], interpolated on the device
+    (include/hdharp.h hd_rfm_attenuate).
+    """
+
+    IPR, ITM = 0, 1
+
+    def __init__(self, options: Optional[AttenuatorOptions] = None):
+        self.options = (options or AttenuatorOptions()).copy()
+        op = self.options
+        if options is None:
+            return
+        if len(op.opacity_files()) != 1:
+            raise RuntimeError("Only one opacity file is allowed")
+        if len(op.species_ids()) != 1:
+            raise RuntimeError("Only one species is allowed")
+        if op.species_ids()[0] < 0:
+            raise RuntimeError(f"Invalid species_id: {op.species_ids()[0]}")
+        if op.type() and op.type() != "rfm":
+            raise RuntimeError(f"Mismatch type: {op.type()}")
+        self.reset()
+
+    @classmethod
+    def from_arrays(cls, wave, pres, tgrid, tref, kdata, species: int = 0) -> "RFM":
+        m = cls()
+        m.options.species_ids([int(species)])
+        m._set(np.asarray(wave, np.float64), np.log(np.asarray(pres, np.float64)),
+               np.asarray(tgrid, np.float64), np.asarray(tref, np.float64),
+               np.asarray(kdata, np.float64))
+        return m
+
+    def _set(self, wave, lnp, tgrid, tref, kdata):
+        nw, npr, nt = len(wave), len(lnp), len(tgrid)
+        if kdata.shape != (nw, npr, nt):
+            raise RuntimeError(f"RFM: table shape {kdata.shape} != {(nw, npr, nt)}")
+        if len(tref) != npr:
+            raise RuntimeError("RFM: reference temperature must have one value per pressure")
+        self.kshape = (nw, npr, nt)
+        self.kaxis = torch.as_tensor(np.concatenate([wave, lnp, tgrid]))
+        self.kdata = torch.as_tensor(np.ascontiguousarray(kdata))
+        self.krefatm = torch.as_tensor(np.stack([lnp, tref]))
+        self._dev_tables = {}
+
+    def reset(self):
+        from .ncread import NetCDFClassic
+        path = find_resource(self.options.opacity_files()[0])
+        nc = NetCDFClassic(path)
+        nw, npr, nt = (nc.dim_len("Wavenumber"), nc.dim_len("Pressure"),
+                       nc.dim_len("TempGrid"))
+        name = self.options.species_names()[self.options.species_ids()[0]]
+        kd = nc.var(name).reshape(nw, npr, nt)
+        self._set(nc.var("Wavenumber").reshape(nw), np.log(nc.var("Pressure").reshape(npr)),
+                  nc.var("TempGrid").reshape(nt), nc.var("Temperature").reshape(npr), kd)
+
+    def _tables(self, dev):
+        key = str(dev)
+        if key not in self._dev_tables:
+            nw, npr, nt = self.kshape
+            ax = _f64(self.kaxis, dev)
+            self._dev_tables[key] = (ax, _f64(self.krefatm[self.ITM], dev), _f64(self.kdata, dev))
+        return self._dev_tables[key]
+
+    def hd_struct(self, dev) -> _lib.HdRfmTable:
+        nw, npr, nt = self.kshape
+        ax, tref, kd = self._tables(dev)
+        p = ax.data_ptr()
+        return _lib.HdRfmTable(nwave=nw, npres=npr, ntemp=nt, wave=p, lnp=p + 8 * nw,
+                               tgrid=p + 8 * (nw + npr), tref=tref.data_ptr(),
+                               kdata=kd.data_ptr(), species=int(self.options.species_ids()[0]))
+
+    def forward(self, conc: torch.Tensor, kwargs: Dict[str, torch.Tensor]) -> torch.Tensor:
+        if "pres" not in kwargs:
+            raise RuntimeError("pres is required in kwargs")
+        if "temp" not in kwargs:
+            raise RuntimeError("temp is required in kwargs")
+        dev = _device(conc, kwargs["pres"], kwargs["temp"])
+        c = _f64(conc, dev)
+        if c.dim() != 3:
+            raise RuntimeError("conc must be (ncol, nlyr, nspecies)")
+        ncol, nlyr, nsp = c.shape
+        p = _f64(kwargs["pres"], dev).expand(ncol, nlyr).contiguous()
+        t = _f64(kwargs["temp"], dev).expand(ncol, nlyr).contiguous()
+        out = torch.empty((self.kshape[0], ncol, nlyr, 1), dtype=torch.float64, device=dev)
+        tab = self.hd_struct(dev)
+        lib = _lib.load()
+        with torch.cuda.device(dev):
+            _lib.check(lib.hd_rfm_attenuate(ctypes.byref(tab), c.data_ptr(), ncol, nlyr, nsp,
+                                            p.data_ptr(), t.data_ptr(), out.data_ptr(),
+                                            torch.cuda.current_stream(dev).cuda_stream))
+        return out if conc.device.type == "cuda" else out.to(conc.device)
+
+    __call__ = forward
+
+
+def read_weights_rfm(filename: str) -> torch.Tensor:
+    """src/utils/read_weights.cpp:18-46: the ``weights`` variable of an RFM ck file."""
+    from .ncread import NetCDFClassic
+    nc = NetCDFClassic(find_resource(filename))
+    n = nc.dim_len("weights")
+    return torch.as_tensor(nc.var("weights").reshape(n).copy())

@@ -183,3 +183,56 @@ def test_cpp_amars_sw(oracle_c, nstr):
     assert rel_err(lev[None], bref).max() < TOL
     href = H.heating_rate(bref, dz, rho, 844.0)[0]
     assert np.abs(lay - href).max() <= 1e-6 * np.abs(href).max()
+
+
+def test_rfm_forward_matches_oracle():
+    """RFM (hd_rfm_attenuate) vs the interpn restatement: pressures and
+    temperatures inside, at and beyond the table nodes (clamped)."""
+    from pyharp_amd.opacity import RFM
+    rng = np.random.default_rng(21)
+    nw, npr, nt = 9, 7, 4
+    wave = np.linspace(10.0, 90.0, nw)
+    pres = np.logspace(6.5, 3, npr)
+    tgrid = np.linspace(-30.0, 30.0, nt)
+    tref = np.linspace(300.0, 180.0, npr)
+    kdata = rng.uniform(-6, 3, (nw, npr, nt))
+    m = RFM.from_arrays(wave, pres, tgrid, tref, kdata, species=1)
+    ncol, nlyr = 3, 11
+    p = np.exp(rng.uniform(np.log(5e2), np.log(8e6), (ncol, nlyr)))
+    p[0, :3] = pres[:3]                        # exactly at pressure nodes
+    t = rng.uniform(120.0, 360.0, (ncol, nlyr))
+    conc = rng.uniform(0.1, 2.0, (ncol, nlyr, 2))
+    got = m.forward(torch.as_tensor(conc, device=DEV),
+                    {"pres": torch.as_tensor(p, device=DEV),
+                     "temp": torch.as_tensor(t, device=DEV)}).cpu().numpy()
+    ref = H.rfm_forward(wave, np.log(pres), tgrid, tref, kdata, conc, p, t, 1)
+    assert got.shape == (nw, ncol, nlyr, 1)
+    np.testing.assert_allclose(got, ref, rtol=1e-13, atol=0)
+
+
+def test_amars_lw_with_rfm_tables(oracle_c, tmp_path):
+    """examples/amars_lw.py --table: amars_lw.cpp:40-88 on a synthetic classic-netCDF
+    RFM file -- RFM optics, Planck solve, ck-weighted band flux -- vs the oracles."""
+    from rfm_fixture import write_rfm_table
+    from pyharp_amd.opacity import add_resource_directory
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "examples"))
+    import amars_lw
+    fx = write_rfm_table(str(tmp_path / "amarsw-ck-B1.nc"))
+    add_resource_directory(str(tmp_path))
+    r = amars_lw.run_rfm("amarsw-ck-B1.nc", nstr=8, nlyr=40)
+    nw = len(fx["wave"])
+    conc = np.ones((1, 40, 2))
+    p = np.full((1, 40), 10.e5)
+    t = np.full((1, 40), 300.0)
+    lnp = np.log(fx["pres"])
+    prop = sum(H.rfm_forward(fx["wave"], lnp, fx["tgrid"], fx["tref"], fx["tables"][sp], conc,
+                             p, t, i) for i, sp in enumerate(("CO2", "H2O")))
+    np.testing.assert_allclose(r["prop"].cpu().numpy(), prop, rtol=1e-13)
+    temf = r["temf"].cpu().numpy()
+    bc = {"albedo": np.ones((nw, 1)), "btemp": np.full((nw, 1), 300.0)}
+    fref = oracle_c.forward(prop, bc, temf, nstr=8, planck=True, wave_lower=np.full(nw, 1.0),
+                            wave_upper=np.full(nw, 150.0))
+    assert rel_err(r["flux"].cpu().numpy(), fref).max() < TOL
+    np.testing.assert_array_equal(r["weights"].cpu().numpy(), fx["weights"])
+    bref = H.band_flux(fref, fx["weights"])
+    assert rel_err(r["bflux"].cpu().numpy()[None], bref[None]).max() < TOL
