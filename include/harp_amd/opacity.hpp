@@ -1,7 +1,9 @@
 // harp_amd/opacity.hpp -- libtorch drop-ins for pyharp's table attenuators
 // (harp::S8Fuller, harp::H2SO4Simple; src/opacity/s8_fuller.cpp,
-// src/opacity/h2so4_simple.cpp) and the SW example's optics assembly
-// (examples/amars_sw.cpp:261-271), backed by libhdisort.so (include/hdharp.h).
+// src/opacity/h2so4_simple.cpp), the RFM absorption tables (harp::RFM,
+// src/opacity/rfm.cpp; tables read from classic netCDF by ncread.hpp),
+// read_weights_rfm (src/utils/read_weights.cpp) and the SW example's optics
+// assembly (examples/amars_sw.cpp:261-271), backed by libhdisort.so (include/hdharp.h).
 //
 //     harp_amd::AttenuatorOptions op;
 //     op.species_names({"S8", "H2SO4"}).species_weights({256.e-3, 98.e-3});
@@ -21,6 +23,7 @@
 #include <torch/nn/module.h>
 #include <torch/torch.h>
 
+#include <cmath>
 #include <cstdlib>
 #include <fstream>
 #include <map>
@@ -30,6 +33,7 @@
 #include <vector>
 
 #include "../hdharp.h"
+#include "ncread.hpp"
 #include "../hdisort.h"
 
 namespace harp_amd {
@@ -235,6 +239,93 @@ torch::Tensor band_optics_of(torch::Tensor conc, torch::Tensor dz,
                              M&... mods) {
   auto dev = detail::device_of({conc, detail::coord_of(kwargs).first, dz});
   return band_optics({mods->table(dev)...}, conc, dz, kwargs, nprop);
+}
+
+// ---- RFM (src/opacity/rfm.hpp, rfm.cpp) -------------------------------------
+class RFMImpl : public torch::nn::Cloneable<RFMImpl> {
+ public:
+  constexpr static int IPR = 0;
+  constexpr static int ITM = 1;
+  size_t kshape[3] = {0, 0, 0};  //! (nwave, npres, ntemp)
+  torch::Tensor kaxis;           //! (nwave + npres + ntemp,): wave, ln p, T anomaly
+  torch::Tensor kdata;           //! (nwave, npres, ntemp) ln(m^2/kmol)
+  torch::Tensor krefatm;         //! (2, npres): ln p, T_ref
+  AttenuatorOptions options;
+
+  RFMImpl() = default;
+  explicit RFMImpl(AttenuatorOptions const& op) : options(op) {
+    TORCH_CHECK(options.opacity_files().size() == 1, "Only one opacity file is allowed");
+    TORCH_CHECK(options.species_ids().size() == 1, "Only one species is allowed");
+    TORCH_CHECK(options.species_ids()[0] >= 0, "Invalid species_id: ", options.species_ids()[0]);
+    TORCH_CHECK(options.type().empty() || options.type() == "rfm", "Mismatch type: ",
+                options.type());
+    reset();
+  }
+
+  void reset() override {
+    NetCDFClassic nc(find_resource(options.opacity_files()[0]));
+    kshape[0] = nc.dim_len("Wavenumber");
+    kshape[1] = nc.dim_len("Pressure");
+    kshape[2] = nc.dim_len("TempGrid");
+    const int nw = (int)kshape[0], np_ = (int)kshape[1], nt = (int)kshape[2];
+    std::vector<double> ax = nc.var("Wavenumber");
+    std::vector<double> pr = nc.var("Pressure");
+    std::vector<double> tg = nc.var("TempGrid");
+    std::vector<double> tr = nc.var("Temperature");
+    TORCH_CHECK((int)ax.size() == nw && (int)pr.size() == np_ && (int)tg.size() == nt &&
+                    (int)tr.size() == np_, "RFM: inconsistent table axes");
+    for (auto& x : pr) x = std::log(x);  // pressure -> ln pressure
+    ax.insert(ax.end(), pr.begin(), pr.end());
+    ax.insert(ax.end(), tg.begin(), tg.end());
+    auto name = options.species_names().at(options.species_ids()[0]);
+    std::vector<double> kd = nc.var(name);
+    TORCH_CHECK((int64_t)kd.size() == (int64_t)nw * np_ * nt, "RFM: table ", name, " size");
+    auto o = torch::TensorOptions().dtype(torch::kFloat64);
+    kaxis = register_buffer("kaxis", torch::tensor(ax, o));
+    kdata = register_buffer("kdata", torch::tensor(kd, o).view({nw, np_, nt}));
+    krefatm = register_buffer("krefatm", torch::stack({torch::tensor(pr, o), torch::tensor(tr, o)}));
+    dev_.clear();
+  }
+
+  //! (nwave, ncol, nlyr, 1) = 1e-3 exp(k) conc; kwargs "pres" [Pa], "temp" [K]: (ncol, nlyr)
+  torch::Tensor forward(torch::Tensor conc, std::map<std::string, torch::Tensor> const& kwargs) {
+    TORCH_CHECK(kwargs.count("pres") > 0, "pres is required in kwargs");
+    TORCH_CHECK(kwargs.count("temp") > 0, "temp is required in kwargs");
+    auto dev = detail::device_of({conc, kwargs.at("pres"), kwargs.at("temp")});
+    auto o = torch::TensorOptions().dtype(torch::kFloat64).device(dev);
+    auto c = conc.to(o).contiguous();
+    TORCH_CHECK(c.dim() == 3, "conc must be (ncol, nlyr, nspecies)");
+    const int ncol = c.size(0), nlyr = c.size(1), nsp = c.size(2);
+    auto p = kwargs.at("pres").to(o).expand({ncol, nlyr}).contiguous();
+    auto t = kwargs.at("temp").to(o).expand({ncol, nlyr}).contiguous();
+    auto out = torch::empty({(int64_t)kshape[0], ncol, nlyr, 1}, o);
+    auto key = dev.str();
+    if (!dev_.count(key))
+      dev_[key] = {kaxis.to(o).contiguous(), krefatm.select(0, ITM).to(o).contiguous(),
+                   kdata.to(o).contiguous()};
+    auto& d = dev_[key];
+    const double* ax = d[0].data_ptr<double>();
+    hd_rfm_table tab{(int)kshape[0], (int)kshape[1], (int)kshape[2], ax, ax + kshape[0],
+                     ax + kshape[0] + kshape[1], d[1].data_ptr<double>(), d[2].data_ptr<double>(),
+                     options.species_ids()[0]};
+    int rc = hd_rfm_attenuate(&tab, c.data_ptr<double>(), ncol, nlyr, nsp, p.data_ptr<double>(),
+                              t.data_ptr<double>(), out.data_ptr<double>(), detail::stream_of(dev));
+    TORCH_CHECK(rc == HD_OK, "hd_rfm_attenuate: ", hd_last_error(nullptr));
+    return conc.is_cuda() ? out : out.to(conc.device());
+  }
+
+ private:
+  std::map<std::string, std::vector<torch::Tensor>> dev_;
+};
+TORCH_MODULE(RFM);
+
+//! src/utils/read_weights.cpp:18-46
+inline torch::Tensor read_weights_rfm(std::string const& filename) {
+  NetCDFClassic nc(find_resource(filename));
+  const size_t n = nc.dim_len("weights");
+  auto w = nc.var("weights");
+  TORCH_CHECK(w.size() == n, "read_weights_rfm: size mismatch");
+  return torch::tensor(w, torch::TensorOptions().dtype(torch::kFloat64));
 }
 
 }  // namespace harp_amd

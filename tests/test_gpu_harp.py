@@ -236,3 +236,31 @@ def test_amars_lw_with_rfm_tables(oracle_c, tmp_path):
     np.testing.assert_array_equal(r["weights"].cpu().numpy(), fx["weights"])
     bref = H.band_flux(fref, fx["weights"])
     assert rel_err(r["bflux"].cpu().numpy()[None], bref[None]).max() < TOL
+
+
+def test_cpp_amars_lw(oracle_c, tmp_path):
+    """tests/cpp/amars_lw_dropin.cpp: amars_lw.cpp's main() against harp_amd::RFM,
+    harp_amd::Disort and harp_amd::read_weights_rfm on a synthetic ck table."""
+    import subprocess
+    from rfm_fixture import write_rfm_table
+    root = os.path.dirname(HERE)
+    exe = os.path.join(root, "tests", "cpp", "amars_lw_dropin")
+    if not os.path.exists(exe):
+        subprocess.run([os.path.join(root, "tests", "cpp", "build.sh")], check=True)
+    fx = write_rfm_table(str(tmp_path / "amarsw-ck-B1.nc"))
+    out = subprocess.run([exe, str(tmp_path)], check=True, capture_output=True,
+                         text=True).stdout.split("\n")
+    prop_c = np.array([float(l.split()[2]) for l in out if l.startswith("prop")])
+    bflx = np.array([[float(x) for x in l.split()[2:]] for l in out if l.startswith("bflx")])
+    nw = len(fx["wave"])
+    conc = np.ones((1, 40, 2))
+    lnp = np.log(fx["pres"])
+    prop = sum(H.rfm_forward(fx["wave"], lnp, fx["tgrid"], fx["tref"], fx["tables"][sp], conc,
+                             np.full((1, 40), 10.e5), np.full((1, 40), 300.0), i)
+               for i, sp in enumerate(("CO2", "H2O")))
+    np.testing.assert_allclose(prop_c, prop[:, 0, 0, 0], rtol=1e-13)
+    bc = {"albedo": np.ones((nw, 1)), "btemp": np.full((nw, 1), 300.0)}
+    fref = oracle_c.forward(prop, bc, np.full((1, 41), 300.0), nstr=8, planck=True,
+                            wave_lower=np.full(nw, 1.0), wave_upper=np.full(nw, 150.0))
+    bref = H.band_flux(fref, fx["weights"])
+    assert rel_err(bflx[None], bref).max() < TOL

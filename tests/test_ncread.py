@@ -85,3 +85,34 @@ def test_interpn_oracle_is_multilinear():
     for pt in ([1.5, 0.0, 12.0], [3.9, 2.9, 19.0], [2.0, 0.5, 10.0]):
         assert abs(H.interpn(pt, data, ax) - f(*pt)) < 1e-12
     assert abs(H.interpn([0.0, -5.0, 30.0], data, ax) - f(1.0, -1.0, 20.0)) < 1e-12
+
+
+def test_cpp_reader_matches(tmp_path):
+    """include/harp_amd/ncread.hpp (compiled with g++ here) reads the same values"""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "ncread_check")
+    subprocess.run(["g++", "-O1", "-std=c++17", "-I", os.path.join(root, "include"),
+                    os.path.join(root, "tests", "cpp", "ncread_check.cpp"), "-o", exe],
+                   check=True)
+    fx = write_rfm_table(str(tmp_path / "ck.nc"), version=1)
+    out = subprocess.run([exe, str(tmp_path / "ck.nc"), "dim:Pressure", "Pressure", "H2O",
+                          "weights"], capture_output=True, text=True, check=True).stdout.split("\n")
+    vals = {}
+    for l in out:
+        if not l:
+            continue
+        parts = l.split()
+        if parts[0].startswith("dim:"):
+            vals[parts[0]] = int(parts[1])
+        else:
+            vals.setdefault(parts[0], []).append(float(parts[2]))
+    assert vals["dim:Pressure"] == 12
+    np.testing.assert_array_equal(vals["Pressure"], fx["pres"])
+    np.testing.assert_array_equal(np.array(vals["H2O"]).reshape(16, 12, 5), fx["tables"]["H2O"])
+    np.testing.assert_array_equal(vals["weights"], fx["weights"])
+    bad = tmp_path / "h.nc"
+    bad.write_bytes(b"\x89HDF\r\n\x1a\n" + b"\0" * 32)
+    r = subprocess.run([exe, str(bad), "x"], capture_output=True, text=True)
+    assert r.returncode == 2 and "HDF5" in r.stdout
