@@ -153,6 +153,7 @@ class DisortImpl : public torch::nn::Cloneable<DisortImpl> {
                   "Disort: planck needs wave_lower/wave_upper of size nwave");
     onlyfl_ = flags.count("onlyfl") > 0;
     usrtau_ = flags.count("usrtau") > 0;
+    corint_ = flags.count("intensity_correction") + flags.count("old_intensity_correction") > 0;
     radiance_ = !onlyfl_ || usrtau_;
     rad_ = torch::Tensor();
     auto& d = options.ds();
@@ -252,7 +253,8 @@ class DisortImpl : public torch::nn::Cloneable<DisortImpl> {
     if (radiance_) {
       auto const& d = options.ds();
       hd_radiance rad{usrtau_ ? d.ntau : 0, d.utau.data(), (int)umu_.size(), umu_.data(),
-                      (int)phi_.size(), phi_.data(), bp("phi0"), onlyfl_ ? 1 : 0};
+                      (int)phi_.size(), phi_.data(), bp("phi0"), onlyfl_ ? 1 : 0,
+                      corint_ ? 1 : 0};
       torch::Tensor uu;
       if (!onlyfl_) uu = torch::empty({nwave, ncol, (int)phi_.size(), d.ntau, (int)umu_.size()}, f64);
       rc = hd_solve_radiance(context(dev.index()), &cfg, &in, &rad, flux.data_ptr<double>(),
@@ -269,7 +271,7 @@ class DisortImpl : public torch::nn::Cloneable<DisortImpl> {
 
  private:
   bool planck_ = false;
-  bool onlyfl_ = true, usrtau_ = false, radiance_ = false;
+  bool onlyfl_ = true, usrtau_ = false, radiance_ = false, corint_ = false;
   std::vector<double> umu_, phi_;
   torch::Tensor rad_;
 

@@ -126,13 +126,15 @@ int hd_solve(hd_context *ctx, const hd_config *cfg, const hd_inputs *in, double 
  *   phi    HOST [nphi] user azimuths [deg]
  *   phi0   DEVICE [nwave*ncol] beam azimuth [deg] or NULL (0)
  *   onlyfl 1: fluxes at the user depths only (uu untouched)
+ *   corint 1: Nakajima-Tanaka TMS correction of the beam's single scattering
+ *          (flag intensity_correction; DISORT 2.0 INTCOR, STWL eq. 68)
  * Outputs (device):
  *   flux [nwave][ncol][ntau][2]  index 0 = the deepest user depth (harp order,
  *        as the level fluxes of hd_solve), [..][0] up, [..][1] rfldir + rfldn
  *   uu   [nwave][ncol][nphi][ntau][numu]  radiance, user order
  *        (cdisort's uu[j][lu][iu] per solve)
- * No Nakajima-Tanaka intensity correction is applied: radiances are the
- * delta-M solution's (identical where the truncation vanishes, chi_nstr = 0).
+ * The IMS secondary-scattering term and cdisort's new correction are not
+ * applied (all corrections vanish where the truncation does, chi_nstr = 0).
  */
 typedef struct hd_radiance {
   int ntau;
@@ -143,6 +145,7 @@ typedef struct hd_radiance {
   const double *phi;
   const double *phi0;
   int onlyfl;
+  int corint;
 } hd_radiance;
 
 int hd_solve_radiance(hd_context *ctx, const hd_config *cfg, const hd_inputs *in,

@@ -31,11 +31,13 @@ c_fluxes        :func:`disort_rad_column` (fluxes at the user depths)
 azimuth sum     uu = sum_m uum cos(m (phi - phi0)), phi in degrees
 ==============  ===========================================================
 
-Not restated: the Nakajima-Tanaka intensity corrections (``intensity_correction``,
-``old_intensity_correction``).  They vanish when the delta-M truncation does
-(f = chi_nstr = 0, e.g. isotropic or Rayleigh phase functions, the
-``tests/test_disort.cpp`` configuration); the parity tests use such phase
-functions wherever intensities are compared.
+Intensity correction: :func:`tms_correction` restates the Nakajima-Tanaka TMS
+step of DISORT 2.0's INTCOR (exact single scattering with the full moment
+series in place of the delta-M one).  Not restated: the IMS secondary-scattering
+term of the old correction and cdisort's new (Buras-Emde-Dowling) correction.
+All of them vanish when the delta-M truncation does (f = chi_nstr = 0, e.g.
+isotropic or Rayleigh phase functions, the ``tests/test_disort.cpp``
+configuration).
 
 Parity status: **parity unpinned** against cdisort (absent).  Pinned by known
 answers in ``tests/test_rad_oracle.py``: quadrature-angle intensities equal the
@@ -52,7 +54,7 @@ import math
 import numpy as np
 import scipy.linalg
 
-from .disort_np import double_gauss, plkavg, setdis, soleig, upisot
+from .disort_np import DITHER, double_gauss, legendre_table, plkavg, setdis, soleig, upisot
 
 
 def lepoly(nstr: int, m: int, mu) -> np.ndarray:
@@ -126,8 +128,11 @@ def _seg_lin(a0, a1, t1, t2, tau, mu):
 def disort_rad_column(dtauc, ssalb, pmom, nstr, *, umu, phi, utau, umu0=1.0, phi0=0.0,
                       fbeam=0.0, albedo=0.0, fisot=0.0, planck=False, temper=None,
                       btemp=0.0, ttemp=0.0, temis=0.0, wvnmlo=0.0, wvnmhi=0.0,
-                      onlyfl=False):
+                      onlyfl=False, corint=False):
     """One DISORT solve with intensities (layers top->bottom, cdisort order).
+
+    corint: the Nakajima-Tanaka TMS correction of the beam's single scattering
+    (see :func:`tms_correction`).
 
     umu: user polar cosines (nonzero), phi: user azimuths [deg], utau: user
     optical depths (unscaled, ascending).  Returns dict with ``uu``
@@ -171,6 +176,9 @@ def disort_rad_column(dtauc, ssalb, pmom, nstr, *, umu, phi, utau, umu0=1.0, phi
                                      fbeam, albedo, fisot, planck, bplanck, tplanck)
     cosm = np.cos(np.outer(np.arange(nmode), np.radians(phi - phi0)))  # (nmode, nphi)
     out["uu"] = np.einsum("mj,mtu->jtu", cosm, uum)
+    if corint and beam and not onlyfl:
+        out["uu"] = out["uu"] + tms_correction(dtauc, ssalb, pmom, nstr, umu, phi, lay, utaupr,
+                                               taucpr, umu0, phi0, fbeam)
     out["uum"] = uum
     return out
 
@@ -337,8 +345,56 @@ def _user_intensity(sol, m, nstr, nn, nlyr, umu, lay, utaupr, cmu, cwt, cmu_full
     return res
 
 
+def _sinsca(phase, omega, taucpr, lay, tau, mu, umu0, fbeam):
+    """Single-scattered beam radiance at scaled depth tau (layer lay) in
+    direction mu, per-layer phase-function values ``phase`` (DISORT SINSCA,
+    STWL eqs. 65b-e)."""
+    nlyr = len(phase)
+    s = 0.0
+    if mu > 0.0:   # from the layers below
+        for lc in range(lay, nlyr):
+            t1, t2 = max(tau, taucpr[lc]), taucpr[lc + 1]
+            s += omega[lc] * phase[lc] * _seg_exp(1.0, 1.0 / umu0, 0.0, t1, t2, tau, mu)
+    else:          # from the layers above
+        for lc in range(lay, -1, -1):
+            t1, t2 = min(tau, taucpr[lc + 1]), taucpr[lc]
+            s += omega[lc] * phase[lc] * _seg_exp(1.0, 1.0 / umu0, 0.0, t1, t2, tau, mu)
+    return fbeam / (4.0 * math.pi) * s
+
+
+def tms_correction(dtauc, ssalb, pmom, nstr, umu, phi, lay, utaupr, taucpr, umu0, phi0, fbeam):
+    """Nakajima-Tanaka TMS correction (DISORT 2.0 INTCOR, STWL eq. 68): replace the
+    delta-M solution's single scattering (truncated phase function with omega')
+    by the exact one (full moment series, omega/(1 - f omega)), both on the
+    scaled optical depths.  Returns the (nphi, ntau, numu) increment."""
+    ssalb = np.where(np.asarray(ssalb, np.float64) == 1.0, 1.0 - DITHER, ssalb)
+    nlyr = len(dtauc)
+    nmom = pmom.shape[1] - 1
+    f = pmom[:, nstr] if nmom >= nstr else np.zeros(nlyr)
+    oprim = ssalb * (1.0 - f) / (1.0 - ssalb * f)
+    out = np.zeros((len(phi), len(utaupr), len(umu)))
+    for j, ph in enumerate(phi):
+        for iu, mu in enumerate(umu):
+            ct = -mu * umu0 + math.sqrt(max(0.0, 1 - mu * mu)) * \
+                math.sqrt(max(0.0, 1 - umu0 * umu0)) * math.cos(math.radians(ph - phi0))
+            pl = legendre_table(nmom + 1, [ct])[:, 0]
+            k = np.arange(nmom + 1)
+            phasa = pmom @ ((2 * k + 1) * pl)                               # (nlyr,)
+            chi = np.zeros((nlyr, nstr))                                    # chi_k, k < nstr
+            chi[:, :min(nstr, nmom + 1)] = pmom[:, :min(nstr, nmom + 1)]
+            kt = np.arange(nstr)
+            plt = legendre_table(nstr, [ct])[:, 0]
+            phasm = ((chi - f[:, None]) / (1.0 - f[:, None])) @ ((2 * kt + 1) * plt)
+            phast = phasa / (1.0 - f * ssalb)
+            for t, (lc, tau) in enumerate(zip(lay, utaupr)):
+                out[j, t, iu] = _sinsca(phast, ssalb, taucpr, lc, tau, mu, umu0, fbeam) - \
+                    _sinsca(phasm, oprim, taucpr, lc, tau, mu, umu0, fbeam)
+    return out
+
+
 def disort_rad_forward(prop, bc, temf=None, *, nstr, umu, phi, utau=None, nmom=None,
-                       planck=False, wave_lower=None, wave_upper=None, onlyfl=False):
+                       planck=False, wave_lower=None, wave_upper=None, onlyfl=False,
+                       corint=False):
     """Batch driver with harp's layout (prop (W, C, L, nprop), layer 0 = bottom).
 
     utau None = the nlyr+1 layer boundaries (top->bottom).  Returns
@@ -378,7 +434,7 @@ def disort_rad_forward(prop, bc, temf=None, *, nstr, umu, phi, utau=None, nmom=N
             r = disort_rad_column(p[:, 0], ssa, pm, nstr, umu=umu, phi=phi, utau=ut,
                                   umu0=v["umu0"][w, c], phi0=v["phi0"][w, c],
                                   fbeam=v["fbeam"][w, c], albedo=v["albedo"][w, c],
-                                  fisot=v["fisot"][w, c], onlyfl=onlyfl, **kw)
+                                  fisot=v["fisot"][w, c], onlyfl=onlyfl, corint=corint, **kw)
             if flux is None:
                 ntau = len(ut)
                 flux = np.zeros((nwave, ncol, ntau, 2))

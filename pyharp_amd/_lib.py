@@ -60,7 +60,8 @@ class HdInputs(ctypes.Structure):
 
 class HdRadiance(ctypes.Structure):
     _fields_ = [("ntau", ctypes.c_int), ("utau", _dp), ("numu", ctypes.c_int), ("umu", _dp),
-                ("nphi", ctypes.c_int), ("phi", _dp), ("phi0", _dp), ("onlyfl", ctypes.c_int)]
+                ("nphi", ctypes.c_int), ("phi", _dp), ("phi0", _dp), ("onlyfl", ctypes.c_int),
+                ("corint", ctypes.c_int)]
 
 
 class HdTiming(ctypes.Structure):

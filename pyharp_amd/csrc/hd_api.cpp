@@ -686,6 +686,7 @@ int hd_solve_radiance(hd_context* ctx, const hd_config* cfg, const hd_inputs* in
     a.numu = numu;
     a.nphi = nphi;
     a.ntau = ntau;
+    a.corint = rad->corint != 0;
     hipError_t e = hd::launch_rad_chunk(nn, a, radiances, stream);
     if (e != hipSuccess)
       return fail(ctx, HD_EHIP, "hd_solve_radiance: launch failed: %s", hipGetErrorString(e));

@@ -1278,6 +1278,89 @@ __global__ __launch_bounds__(256) void hd_rad_azimuth_kernel(RadArgs A) {
   A.uu[(((size_t)s * A.nphi + j) * A.ntau + lu) * A.numu + iu] = acc;
 }
 
+
+// ============================================================================
+// Nakajima-Tanaka TMS correction (DISORT 2.0 INTCOR, STWL eq. 68): exact single
+// scattering (full moment series, omega/(1 - f omega)) minus the delta-M one
+// (truncated series, omega'), both on the scaled depths; added to uu
+// ============================================================================
+__global__ __launch_bounds__(256) void hd_rad_tms_kernel(RadArgs A, int nstr) {
+  const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long n = (long)A.ns * A.nphi * A.ntau * A.numu;
+  if (id >= n) return;
+  const int sl = (int)(id % A.ns);
+  long r = id / A.ns;
+  const int iu = (int)(r % A.numu);
+  r /= A.numu;
+  const int lu = (int)(r % A.ntau);
+  const int j = (int)(r / A.ntau);
+  const long s = A.s0 + sl;
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
+  const double fb = A.fbeam ? A.fbeam[s] : 0.0;
+  if (!(fb > 0.0 && mu0 > 0.0)) return;
+  const int L = A.nlyr, np = A.nprop, nm = A.nmom;
+  const double mu = A.umu[iu];
+  const double ph0 = A.phi0 ? A.phi0[s] : 0.0;
+  const double ct = fma(-mu, mu0, sqrt(fmax(0.0, 1.0 - mu * mu)) *
+                                      sqrt(fmax(0.0, 1.0 - mu0 * mu0)) *
+                                      cos((A.phi[j] - ph0) * (kPi / 180.0)));
+  // user depth -> layer and scaled depth
+  const double tu = user_tau(A, lu, sl);
+  int lu_l = 0;
+  while (lu_l < L - 1 && tu > A.taus[(size_t)(lu_l + 1) * A.ns + sl]) ++lu_l;
+  const double rmu0 = 1.0 / mu0;
+  double acc = 0.0, tau_u = 0.0;
+  for (int pass = 0; pass < 2; ++pass) {  // pass 0: scaled depth of the user level
+    const int lo = pass == 0 ? lu_l : (mu > 0.0 ? lu_l : 0);
+    const int hi = pass == 0 ? lu_l : (mu > 0.0 ? L - 1 : lu_l);
+    for (int lc = lo; lc <= hi; ++lc) {
+      const double* q = A.prop + ((size_t)s * L + (L - 1 - lc)) * np;
+      const double tau = q[0];
+      double ssa = np > 1 ? q[1] : 0.0;
+      if (ssa == 1.0) ssa = 1.0 - kDither;
+      const double f = nm >= nstr ? q[1 + nstr] : 0.0;
+      const double taup = (1.0 - ssa * f) * tau;
+      const double top = A.tauc[(size_t)lc * A.ns + sl];
+      if (pass == 0) {
+        const double ttop = A.taus[(size_t)lc * A.ns + sl];
+        const double scale = tau > 0.0 ? taup / tau : 0.0;
+        tau_u = top + fmin(fmax((tu - ttop) * scale, 0.0), taup);
+        continue;
+      }
+      const double bot = top + taup;
+      const double t1 = mu > 0.0 ? fmax(tau_u, top) : fmin(tau_u, bot);
+      const double t2 = mu > 0.0 ? bot : top;
+      // phase functions at cos(Theta): full series and delta-M truncated series
+      double pa = 1.0, pm = 1.0;  // k = 0 terms: chi_0 = 1, (chi_0 - f)/(1 - f) = 1
+      double p1 = 1.0, p2 = 0.0;
+      const int kmax = nm > nstr - 1 ? nm : nstr - 1;
+      for (int k = 1; k <= kmax; ++k) {
+        const double pk = ((2 * k - 1) * ct * p1 - (k - 1) * p2) / k;
+        p2 = p1;
+        p1 = pk;
+        const double chi = k <= nm ? q[1 + k] : 0.0;
+        if (k <= nm) pa = fma((2 * k + 1) * chi, pk, pa);
+        if (k < nstr) pm = fma((2 * k + 1) * (chi - f) / (1.0 - f), pk, pm);
+      }
+      const double om = ssa * (1.0 - f) / (1.0 - ssa * f);
+      const double w = ssa * pa / (1.0 - f * ssa) - om * pm;
+      // int_{t1}^{t2} e^{-t/mu0} e^{-(t - tau_u)/mu} dt/mu
+      const double e1 = exp(-t1 * rmu0 - (t1 - tau_u) / mu);
+      const double den = fma(rmu0, mu, 1.0);
+      const double x = den * (t2 - t1) / mu;
+      double seg;
+      if (fabs(x) < 0.5) {
+        const double phx = x == 0.0 ? 1.0 : -expm1(-x) / x;
+        seg = e1 * (t2 - t1) / mu * phx;
+      } else {
+        seg = (e1 - exp(-t2 * rmu0 - (t2 - tau_u) / mu)) / den;
+      }
+      acc = fma(w, seg, acc);
+    }
+  }
+  A.uu[(((size_t)s * A.nphi + j) * A.ntau + lu) * A.numu + iu] += fb / (4.0 * kPi) * acc;
+}
+
 // ============================================================================
 // host side
 // ============================================================================
@@ -1362,6 +1445,9 @@ static void launch_rad(const RadArgs& a, bool radiances, hipStream_t st) {
     const long na = (long)a.ns * a.nphi * a.ntau * a.numu;
     hipLaunchKernelGGL(hd_rad_azimuth_kernel, dim3((unsigned)((na + 255) / 256)), dim3(256), 0,
                        st, a);
+    if (a.corint && a.tauc)
+      hipLaunchKernelGGL(hd_rad_tms_kernel, dim3((unsigned)((na + 255) / 256)), dim3(256), 0, st,
+                         a, 2 * NN);
   }
 }
 

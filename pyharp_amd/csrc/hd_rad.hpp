@@ -63,6 +63,7 @@ struct RadArgs {
   int planck;
   int max_sweeps;
   int numu, nphi, ntau;
+  int corint;  // Nakajima-Tanaka TMS correction of the single scattering
 };
 
 hipError_t upload_rad_tables(const QuadHost* per_nn);  // nn 1..kRadMaxNN

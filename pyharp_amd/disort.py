@@ -145,6 +145,9 @@ class Disort(RTSolver):
         self.usrtau = "usrtau" in flags
         self.usrang = "usrang" in flags
         self.radiance = (not self.onlyfl) or self.usrtau
+        # Nakajima-Tanaka TMS correction (either correction flag; the IMS term and
+        # cdisort's new method are not applied -- DESIGN.md section 8)
+        self.corint = bool(flags & {"intensity_correction", "old_intensity_correction"})
         self._rad = None
         if self.radiance:
             if ds.nstr > 16:
@@ -299,7 +302,7 @@ class Disort(RTSolver):
                               numu=len(self._umu), umu=ctypes.cast(mu, ctypes.c_void_p),
                               nphi=len(self._phi), phi=ctypes.cast(ph, ctypes.c_void_p),
                               phi0=phi0.data_ptr() if phi0 is not None else None,
-                              onlyfl=int(self.onlyfl))
+                              onlyfl=int(self.onlyfl), corint=int(self.corint))
         uu = None
         if not self.onlyfl:
             uu = torch.empty((nwave, ncol, len(self._phi), ds.ntau, len(self._umu)), dtype=f64,

@@ -224,3 +224,31 @@ def test_cpp_disort_rad():
     assert abs(flux[1][0] - c["flup"][0]) <= 5e-6 * c["flup"][0]
     dn_bot = c["rfldir"][1] + c["rfldn"][1]
     assert abs(flux[0][1] - dn_bot) <= 5e-6 * dn_bot
+
+
+@pytest.mark.parametrize("nstr", [8, 16])
+def test_tms_corrected_radiances_vs_oracle(nstr):
+    """intensity_correction on forward-peaked HG layers with 48 moments (delta-M
+    truncation active): the TMS-corrected radiances vs the oracle's"""
+    rng = np.random.default_rng(600 + nstr)
+    nwave, ncol, nlyr, nmom = 2, 2, 5, 48
+    prop = np.zeros((nwave, ncol, nlyr, 2 + nmom))
+    prop[..., 0] = 10.0 ** rng.uniform(-3, 0.5, (nwave, ncol, nlyr))
+    prop[..., 1] = rng.uniform(0.3, 0.99, (nwave, ncol, nlyr))
+    g = rng.uniform(0.6, 0.85, (nwave, ncol, nlyr))
+    for l in range(nmom):
+        prop[..., 2 + l] = g ** (l + 1)
+    bc = {"fbeam": np.ones((nwave, ncol)), "umu0": rng.uniform(0.2, 1, (nwave, ncol)),
+          "phi0": rng.uniform(0, 360, (nwave, ncol)), "albedo": rng.uniform(0, 1, (nwave, ncol))}
+    total = prop[..., 0].sum(axis=-1).min()
+    utau = [0.0, 0.5 * total, total]
+    umu, phi = [-0.9, -0.4, 0.3, 0.8], [0.0, 60.0, 180.0]
+    d = _disort(nstr, nlyr, nwave, ncol, flags="usrtau,usrang,lamber,intensity_correction,"
+                "old_intensity_correction", umu=umu, phi=phi, utau=utau, nmom=nmom)
+    d.forward(torch.as_tensor(prop, device=DEV), _dev(bc))
+    uu = d.get_rad().cpu().numpy()
+    _, uref = disort_rad_forward(prop, bc, nstr=nstr, nmom=nmom, umu=umu, phi=phi, utau=utau,
+                                 corint=True)
+    _, u0 = disort_rad_forward(prop, bc, nstr=nstr, nmom=nmom, umu=umu, phi=phi, utau=utau)
+    assert _col_err(uu, uref) < TOL
+    assert _col_err(uref, u0) > 1e-3   # the correction is not a no-op here

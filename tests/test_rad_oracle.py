@@ -222,3 +222,51 @@ def test_disotest1_intensities(case):
                           phi=[0.0], utau=[0.0, c["tau"]], umu0=0.1, fbeam=math.pi / 0.1)
     exp = np.asarray(c["uu"])
     assert np.all(np.abs(r["uu"][0] - exp) <= 5e-6 * np.abs(exp) + 1e-6)
+
+
+def test_tms_restores_exact_single_scattering():
+    """Thin Henyey-Greenstein layer (g = 0.75, 64 moments) with delta-M at nstr 8:
+    the TMS-corrected radiance is the single scattering of the full phase
+    function; the uncorrected delta-M radiance is not."""
+    tau, om, g, nmom = 1e-5, 0.9, 0.75, 64
+    pm = np.array([[g ** l for l in range(nmom + 1)]])
+    umu0, phi0, fbeam = 0.5, 0.0, 1.0
+    umu = np.array([-0.8, -0.3, 0.2, 0.7])
+    phi = np.array([0.0, 90.0, 180.0])
+    kw = dict(umu=umu, phi=phi, utau=[0.0, tau], umu0=umu0, phi0=phi0, fbeam=fbeam)
+    r = disort_rad_column([tau], [om], pm, 8, corint=True, **kw)
+    r0 = disort_rad_column([tau], [om], pm, 8, corint=False, **kw)
+
+    def hg(ct):
+        return (1 - g * g) / (1 + g * g - 2 * g * ct) ** 1.5
+
+    worst_c = worst_0 = 0.0
+    for j, ph in enumerate(phi):
+        for iu, mu in enumerate(umu):
+            ct = -mu * umu0 + math.sqrt(1 - mu * mu) * math.sqrt(1 - umu0 ** 2) * \
+                math.cos(math.radians(ph - phi0))
+            if mu > 0:
+                k = 0
+                exp = om * fbeam / (4 * math.pi) * hg(ct) * umu0 / (umu0 + mu) * \
+                    -math.expm1(-tau * (1 / umu0 + 1 / mu))
+            else:
+                k = 1
+                am = -mu
+                exp = om * fbeam / (4 * math.pi) * hg(ct) * umu0 / (umu0 - am) * \
+                    (math.exp(-tau / umu0) - math.exp(-tau / am))
+            worst_c = max(worst_c, abs(r["uu"][j, k, iu] / exp - 1))
+            worst_0 = max(worst_0, abs(r0["uu"][j, k, iu] / exp - 1))
+    assert worst_c < 1e-4, worst_c
+    assert worst_0 > 1e-2, worst_0      # the correction matters here
+
+
+def test_tms_vanishes_without_truncation():
+    rng = np.random.default_rng(9)
+    nstr, nlyr = 8, 3
+    dtauc, ssalb, pm = _random_column(rng, nlyr, nstr, iso=True)
+    pm[:, 2] = 0.1                                   # Rayleigh: f = chi_8 = 0
+    kw = dict(umu=[-0.5, 0.4], phi=[0.0, 120.0], utau=[0.0, 0.3 * dtauc.sum()], umu0=0.6,
+              fbeam=1.0, albedo=0.3)
+    a = disort_rad_column(dtauc, ssalb, pm, nstr, corint=True, **kw)["uu"]
+    b = disort_rad_column(dtauc, ssalb, pm, nstr, corint=False, **kw)["uu"]
+    np.testing.assert_allclose(a, b, rtol=1e-12, atol=1e-15)
