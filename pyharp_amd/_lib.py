@@ -73,10 +73,14 @@ _lib = None
 
 
 def load(path: str = LIB_PATH):
-    """Load libhdisort.so; raises OSError if it has not been built."""
+    """Load libhdisort.so; raises OSError if it has not been built.
+
+    HD_LIB_PATH overrides the path (A/B runs of kernel variants built
+    out of tree by mb/build_variant.sh)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = os.environ.get("HD_LIB_PATH", path)
     if not os.path.exists(path):
         raise OSError(f"pyharp_amd: {path} not found -- build it with "
                       "`python -m pyharp_amd._build` (hipcc, gfx950); there is no CPU fallback")
