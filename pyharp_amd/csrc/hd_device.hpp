@@ -292,4 +292,97 @@ __device__ __forceinline__ void jacobi_eig(double (&a)[NN][NN], double (&v)[NN][
   }
 }
 
+// ----------------------------------------------------------------------------
+// One-sided (Hestenes) Jacobi on the columns of B, Sym = B^T B.  A rotation of
+// the column pair (p, q) is exactly the two-sided rotation of B^T B for that
+// pair, with a_pp = |b_p|^2 and a_qq = |b_q|^2 tracked (exact at every sweep
+// start) and a_pq = b_p.b_q formed from the columns, so Sym is never formed and
+// the rotations are not accumulated: with B = B0 V the eigenvectors are
+// V = B0^-1 B afterwards (two triangular solves in the layer kernel), and
+// k^2 = |b_j|^2.  Per rotation: 2 NN fma for the dot product, 4 NN ops for the
+// columns -- against 2(NN-2) + 2 NN mul/fma pairs for the two-sided update of
+// Sym and V.  Same tournament ordering and parameter formulas as jacobi_round.
+// ----------------------------------------------------------------------------
+template <int NN>
+__device__ __forceinline__ void jacobi_os_round(int r, double (&b)[NN][NN], double (&nrm)[NN],
+                                                bool on, double& off) {
+  constexpr int P = NN + (NN & 1);
+  constexpr int H = P / 2;
+  double cc[H], ss[H], gg[H];
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    const int x = tour_a(P, r, k), y = tour_b(P, r, k);
+    const int p = x < y ? x : y, q = x < y ? y : x;
+    if (q >= NN) continue;
+    double g0 = 0.0, g1 = 0.0;  // two chains
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      if (i % 2 == 0) g0 = fma(b[i][p], b[i][q], g0);
+      else g1 = fma(b[i][p], b[i][q], g1);
+    }
+    const double gam = g0 + g1;
+    const double app = nrm[p], aqq = nrm[q];
+    const double g2 = gam * gam;
+    off += g2;
+    const bool rot = on && g2 > 1.0e-30 * (app * aqq);
+    // w = sqrt(d^2 + 4 g^2), u = |d| + w, z = 1/sqrt(2 w u): c = u z, s = sgn(d) 2 g z
+    const double d = aqq - app;
+    const double w2 = rot ? fma(d, d, 4.0 * g2) : 1.0;
+    const double w = w2 * rsq_nr1(w2);
+    const double u = fabs(d) + w;
+    const double z = rsq_nr1(2.0 * w * u);
+    const double sg = d < 0.0 ? -2.0 : 2.0;
+    cc[k] = rot ? u * z : 1.0;
+    ss[k] = rot ? sg * gam * z : 0.0;
+    gg[k] = gam;
+  }
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    const int x = tour_a(P, r, k), y = tour_b(P, r, k);
+    const int p = x < y ? x : y, q = x < y ? y : x;
+    if (q >= NN) continue;
+    const double c = cc[k], s = ss[k];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      const double bp = b[i][p], bq = b[i][q];
+      b[i][p] = fma(-s, bq, c * bp);
+      b[i][q] = fma(s, bp, c * bq);
+    }
+    // |c b_p - s b_q|^2 and |s b_p + c b_q|^2
+    const double app = nrm[p], aqq = nrm[q];
+    const double c2 = c * c, s2 = s * s, cs2 = 2.0 * c * s * gg[k];
+    nrm[p] = fma(c2, app, fma(s2, aqq, -cs2));
+    nrm[q] = fma(s2, app, fma(c2, aqq, cs2));
+  }
+}
+
+// Sweeps until the sweep in which the off-diagonal Frobenius norm of B^T B
+// (accumulated from the pairs' b_p.b_q as they were rotated) stayed below
+// 1e-8 of its diagonal: quadratic convergence leaves ~1e-16 after it (the
+// criterion of jacobi_eig, measured one sweep earlier).  A converged lane stops
+// rotating (exact no-ops: c = 1, s = 0), so its result does not depend on which
+// solves share its wave; the loop exits when every lane has converged.
+template <int NN>
+__device__ __forceinline__ void jacobi_os(double (&b)[NN][NN], int max_sweeps) {
+  if constexpr (NN > 1) {
+    constexpr int P = NN + (NN & 1);
+    bool on = true;
+    for (int sweep = 0; sweep < max_sweeps; ++sweep) {
+      double nrm[NN], dia = 0.0, off = 0.0;
+#pragma unroll
+      for (int j = 0; j < NN; ++j) {
+        double t = 0.0;
+#pragma unroll
+        for (int i = 0; i < NN; ++i) t = fma(b[i][j], b[i][j], t);
+        nrm[j] = t;
+        dia = fma(t, t, dia);
+      }
+#pragma unroll
+      for (int r = 0; r < P - 1; ++r) jacobi_os_round<NN>(r, b, nrm, on, off);
+      on = on && off > 1.0e-16 * dia;
+      if (__all(!on)) break;
+    }
+  }
+}
+
 }  // namespace hd

@@ -105,7 +105,8 @@ __global__ __launch_bounds__(256) void hd_tauc_kernel(TaucArgs A) {
 template <int NN>
 __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
   constexpr int N = 2 * NN;
-  constexpr int kPsi = NN > 1 ? NN * NN : 1;
+  // Psi^T staging; also holds L while the Jacobi runs (NN = 2: 5 > 4 doubles)
+  constexpr int kPsi = NN > 1 ? (NN == 2 ? 5 : NN * NN) : 1;
   __shared__ double psi_lds[kPsi * kLayerBlock];  // Psi^T staged per lane
   const Quad<NN>& Qc = quad<NN>();
   // block = 64 consecutive solves (one wave each) x kLayersPerBlock consecutive
@@ -228,6 +229,7 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
       lxd[i] = Qc.sd[i] * xdi;
     }
     lower_solve<NN>(lch, rdl, y2);
+    lower_t_solve<NN>(lch, rdl, y2);  // L^-T y2: V^T y2 = U^T L^-T y2 below
     lower_solve<NN>(lch, rdl, lxd);   // lxd = L^-T L^-1 D^1/2 xd
     lower_t_solve<NN>(lch, rdl, lxd);
   } else {
@@ -256,37 +258,75 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
     for (int i = 0; i < NN; ++i) cvec[i] = 0.0;
   }
 
-  // ---- Sym = L^T (-A+) L (upper), built column by column ----
-  double sym[NN][NN];
+  // ---- eigenpairs (c_soleig): Sym = L^T (-A+) L = V diag(k^2) V^T ----
+  // With C C^T = -A+ (SPD exactly when Sym is), Sym = B^T B for B = C^T L: the
+  // one-sided Jacobi on B's columns gives k^2 = |b_j|^2 and B = B0 V, so
+  // U = L V = C^-T B comes from one triangular solve (it is all the beam and
+  // Omega need; V = L^-1 U only feeds Psi).  Sym itself is never formed.
+  double rdc[NN];
+  if (!chol_inplace<NN>(ap, rdc)) st |= kStEigen;  // lower ap <- C
+  double v[NN][NN];  // B, then U = L V, then Omega = U Delta^1/2
 #pragma unroll
-  for (int j = 0; j < NN; ++j) {
-    double mcol[NN];
+  for (int i = 0; i < NN; ++i)
+#pragma unroll
+    for (int j = 0; j < NN; ++j) {  // B_ij = sum_{k >= max(i,j)} C_ki L_kj
+      double t = 0.0;
+#pragma unroll
+      for (int k = (i > j ? i : j); k < NN; ++k) t = fma(ap[k][i], lch[k][j], t);
+      v[i][j] = t;
+    }
+  // L is not needed again until the beam solution: park it in this lane's (not
+  // yet used) Psi staging area of LDS while B, C and the rotation temporaries
+  // hold the registers.  This keeps the kernel under 464 VGPR+AGPR, so that the
+  // previous chunk's 44-VGPR back-substitution waves still fit beside it on
+  // every SIMD (hd_solve's side stream).
+  constexpr int kPark = NN * (NN + 1) / 2 + NN;
+  static_assert(kPark <= kPsi || NN == 1, "L does not fit the Psi staging area");
+  if constexpr (NN > 1) {
+    int e = 0;
 #pragma unroll
     for (int i = 0; i < NN; ++i) {
-      double t = 0.0;
 #pragma unroll
-      for (int k = j; k < NN; ++k) t = fma(HD_SYM(ap, i, k), lch[k][j], t);
-      mcol[i] = t;
-    }
-#pragma unroll
-    for (int i = 0; i <= j; ++i) {
-      double t = 0.0;
-#pragma unroll
-      for (int k = i; k < NN; ++k) t = fma(lch[k][i], mcol[k], t);
-      sym[i][j] = t;
+      for (int k = 0; k <= i; ++k) psi_lds[(e++) * kLayerBlock + lt] = lch[i][k];
+      psi_lds[(e++) * kLayerBlock + lt] = rdl[i];
     }
   }
-
-  // ---- eigenpairs (c_soleig): Sym = V diag(k^2) V^T ----
-  double v[NN][NN];
-  jacobi_eig<NN>(sym, v, A.max_sweeps);
+  asm volatile("" ::: "memory");
+  HD_PHASE();
+  jacobi_os<NN>(v, A.max_sweeps);
+  HD_PHASE();
   double kk[NN];
 #pragma unroll
   for (int j = 0; j < NN; ++j) {
-    const double k2 = sym[j][j];
+    double k2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < NN; ++i) k2 = fma(v[i][j], v[i][j], k2);
     if (!(k2 > 0.0)) st |= kStEigen;
     kk[j] = sqrt(k2 > 0.0 ? k2 : 0.0);
   }
+#pragma unroll
+  for (int j = 0; j < NN; ++j) {  // U = C^-T B, column by column
+    double x[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) x[i] = v[i][j];
+    lower_t_solve<NN>(ap, rdc, x);
+#pragma unroll
+    for (int i = 0; i < NN; ++i) v[i][j] = x[i];
+  }
+  HD_PHASE();
+  if constexpr (NN > 1) {  // L back from LDS
+    // the empty asm with a memory clobber makes this a real reload (not the
+    // parked registers kept live across the Jacobi) and keeps it in place
+    asm volatile("" ::: "memory");
+    int e = 0;
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+#pragma unroll
+      for (int k = 0; k <= i; ++k) lch[i][k] = psi_lds[(e++) * kLayerBlock + lt];
+      rdl[i] = psi_lds[(e++) * kLayerBlock + lt];
+    }
+  }
+  HD_PHASE();
 
   // ---- beam particular solution Z+/- (c_upbeam), unit attenuation above ----
   double zp[NN], zm[NN];
@@ -308,17 +348,10 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
     }
     double sv[NN], y[NN];
 #pragma unroll
-    for (int i = 0; i < NN; ++i) {  // y = V tt
+    for (int i = 0; i < NN; ++i) {  // s = W^-1 D^1/2 L V tt = W^-1 D^1/2 U tt
       double t = 0.0;
 #pragma unroll
       for (int j = 0; j < NN; ++j) t = fma(v[i][j], tt[j], t);
-      y[i] = t;
-    }
-#pragma unroll
-    for (int i = 0; i < NN; ++i) {  // s = W^-1 D^1/2 L y
-      double t = 0.0;
-#pragma unroll
-      for (int k = 0; k <= i; ++k) t = fma(lch[i][k], y[k], t);
       sv[i] = Qc.rg[i] * t;
     }
     // dd = (lxd - D^1/2 L^-T L^-1 D^1/2 (mu s) / mu0) / w
@@ -352,26 +385,22 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
     dsq[j] = sqrt(delta);
     gsq[j] = sqrt(kk[j] * th);
   }
-  // Psi^T = L^-T V Gamma^1/2 -> LDS (one column per step)
+  // Psi^T = L^-T V Gamma^1/2 = L^-T L^-1 U Gamma^1/2 -> LDS (one column per step)
 #pragma unroll
   for (int j = 0; j < NN; ++j) {
     double x[NN];
 #pragma unroll
     for (int i = 0; i < NN; ++i) x[i] = v[i][j];
+    lower_solve<NN>(lch, rdl, x);
     lower_t_solve<NN>(lch, rdl, x);
 #pragma unroll
     for (int i = 0; i < NN; ++i) psi_lds[(i * NN + j) * kLayerBlock + lt] = x[i] * gsq[j];
   }
-  // Omega = L V Delta^1/2, in place over v (rows bottom-up)
+  // Omega = L V Delta^1/2 = U Delta^1/2, in place over v
 #pragma unroll
-  for (int i = NN - 1; i >= 0; --i)
+  for (int i = 0; i < NN; ++i)
 #pragma unroll
-    for (int j = 0; j < NN; ++j) {
-      double t = 0.0;
-#pragma unroll
-      for (int a = 0; a <= i; ++a) t = fma(lch[i][a], v[a][j], t);
-      v[i][j] = t * dsq[j];
-    }
+    for (int j = 0; j < NN; ++j) v[i][j] *= dsq[j];
 
   double* out = A.scr + (size_t)lc * ne1<NN>() * A.nsc + sl;
   const size_t so = A.nsc;
