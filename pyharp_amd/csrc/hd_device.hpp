@@ -195,6 +195,34 @@ __device__ __forceinline__ void lower_t_solve(const double (&l)[NN][NN], const d
   }
 }
 
+// (L L^T)^-1 from the Cholesky factor left in the lower triangle of a (rd =
+// 1/diag(L)): K = L^-1 (lower, NN^3/6 fma), then inv = K^T K written into the
+// upper triangle of a (diagonal included; L's diagonal is not needed again).
+template <int NN>
+__device__ __forceinline__ void spd_inverse_upper(double (&a)[NN][NN], const double (&rd)[NN]) {
+  double k[NN][NN];  // lower
+#pragma unroll
+  for (int j = 0; j < NN; ++j) {
+    k[j][j] = rd[j];
+#pragma unroll
+    for (int i = j + 1; i < NN; ++i) {
+      double t = 0.0;
+#pragma unroll
+      for (int m = j; m < i; ++m) t = fma(a[i][m], k[m][j], t);
+      k[i][j] = -t * rd[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NN; ++i)
+#pragma unroll
+    for (int j = i; j < NN; ++j) {
+      double t = 0.0;
+#pragma unroll
+      for (int m = j; m < NN; ++m) t = fma(k[m][i], k[m][j], t);
+      a[i][j] = t;
+    }
+}
+
 // ----------------------------------------------------------------------------
 // Jacobi eigensolver, parallel (round-robin tournament) ordering: a sweep is
 // P-1 rounds of P/2 disjoint rotations (P = NN rounded up to even).  The

@@ -411,78 +411,61 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
     ga[i] = Qc.g[i] * (cvec[i] - fma(-zp[i], e0, zm[i]));
     gb[i] = Qc.g[i] * (fma(zp[i], e0, zm[i]) + bsum);
   }
-  // Q~- = Omega (I + Omega^T Omega)^-1 Omega^T = Phi Phi^T, Phi = Omega J^-T
-  double pvec[NN], qmr[NN][NN];
+  // By Woodbury, Q~- = Omega (I + Omega^T Omega)^-1 Omega^T = I - A-  and
+  // Q~+ = -Psi^T (I + Psi Psi^T)^-1 Psi = A+ - I  with the SPD inverses
+  // A- = (I + Omega Omega^T)^-1, A+ = (I + Psi^T Psi)^-1 (eigenvalues in (0, 1]),
+  // so R~ = A+ - A-, T~ = A- + A+ - I and the sources need A-/A+ times a vector.
+  double pvec[NN], am_[NN][NN];
   {
-    double hm[NN][NN], rdh[NN];
 #pragma unroll
     for (int i = 0; i < NN; ++i)
 #pragma unroll
       for (int j = i; j < NN; ++j) {
         double t = (i == j) ? 1.0 : 0.0;
 #pragma unroll
-        for (int k = 0; k < NN; ++k) t = fma(v[k][i], v[k][j], t);
-        hm[i][j] = t;
-      }
-    if (!chol_inplace<NN>(hm, rdh)) st |= kStEigen;
-#pragma unroll
-    for (int r = 0; r < NN; ++r) lower_solve<NN>(hm, rdh, v[r]);
-    // Q~- (upper, kept in registers); p = Q~- ga
-#pragma unroll
-    for (int i = 0; i < NN; ++i) pvec[i] = 0.0;
-#pragma unroll
-    for (int i = 0; i < NN; ++i)
-#pragma unroll
-      for (int j = i; j < NN; ++j) {
-        double t = 0.0;
-#pragma unroll
         for (int k = 0; k < NN; ++k) t = fma(v[i][k], v[j][k], t);
-        qmr[i][j] = t;
-        pvec[i] = fma(t, ga[j], pvec[i]);
-        if (j != i) pvec[j] = fma(t, ga[i], pvec[j]);
+        am_[i][j] = t;
       }
+    double rdh[NN];
+    if (!chol_inplace<NN>(am_, rdh)) st |= kStEigen;
+    spd_inverse_upper<NN>(am_, rdh);
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {  // p = Q~- ga = ga - A- ga
+      double t = ga[i];
+#pragma unroll
+      for (int j = 0; j < NN; ++j) t = fma(-HD_SYM(am_, i, j), ga[j], t);
+      pvec[i] = t;
+    }
   }
-  // Q~+ = -Psi^T (I + Psi Psi^T)^-1 Psi = -Xi^T Xi, Xi = J+^-1 Psi
-  double qp[NN][NN];
+  double ap_[NN][NN], qvec[NN];
   {
     double pt_[NN][NN];  // pt_[i][j] = Psi^T[i][j]
 #pragma unroll
     for (int i = 0; i < NN; ++i)
 #pragma unroll
       for (int j = 0; j < NN; ++j) pt_[i][j] = psi_lds[(i * NN + j) * kLayerBlock + lt];
-    double hp[NN][NN], rdh[NN];
 #pragma unroll
     for (int i = 0; i < NN; ++i)
 #pragma unroll
       for (int j = i; j < NN; ++j) {
         double t = (i == j) ? 1.0 : 0.0;
 #pragma unroll
-        for (int k = 0; k < NN; ++k) t = fma(pt_[k][i], pt_[k][j], t);
-        hp[i][j] = t;
-      }
-    if (!chol_inplace<NN>(hp, rdh)) st |= kStEigen;
-#pragma unroll
-    for (int r = 0; r < NN; ++r) lower_solve<NN>(hp, rdh, pt_[r]);
-#pragma unroll
-    for (int i = 0; i < NN; ++i)
-#pragma unroll
-      for (int j = i; j < NN; ++j) {
-        double t = 0.0;
-#pragma unroll
         for (int k = 0; k < NN; ++k) t = fma(pt_[i][k], pt_[j][k], t);
-        qp[i][j] = -t;
+        ap_[i][j] = t;
       }
-  }
-  double qvec[NN];
+    double rdh[NN];
+    if (!chol_inplace<NN>(ap_, rdh)) st |= kStEigen;
+    spd_inverse_upper<NN>(ap_, rdh);
 #pragma unroll
-  for (int i = 0; i < NN; ++i) {
-    double t = 0.0;
+    for (int i = 0; i < NN; ++i) {  // q = Q~+ gb = A+ gb - gb
+      double t = -gb[i];
 #pragma unroll
-    for (int j = 0; j < NN; ++j) t = fma(HD_SYM(qp, i, j), gb[j], t);
-    qvec[i] = t;
+      for (int j = 0; j < NN; ++j) t = fma(HD_SYM(ap_, i, j), gb[j], t);
+      qvec[i] = t;
+    }
   }
 
-  // ---- store: R~ = Q~- + Q~+, T~ = I - Q~- + Q~+ (upper), S~+, S~-, tau' ----
+  // ---- store: R~ = A+ - A-, T~ = A- + A+ - I (upper), S~+, S~-, tau' ----
   double chk = 0.0;
   {
     int e = 0;
@@ -490,9 +473,8 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
     for (int i = 0; i < NN; ++i)
 #pragma unroll
       for (int j = i; j < NN; ++j) {
-        const double qm = qmr[i][j];
-        const double r = qm + qp[i][j];
-        const double t = ((i == j) ? 1.0 : 0.0) - qm + qp[i][j];
+        const double r = ap_[i][j] - am_[i][j];
+        const double t = (am_[i][j] + ap_[i][j]) - ((i == j) ? 1.0 : 0.0);
         out[e * so] = r;
         out[(nsym + e) * so] = t;
         chk += r + t;

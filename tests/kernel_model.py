@@ -7,11 +7,14 @@ never imported by the product.
 
 Formulation:
   * homogeneous solution from the symmetrised eigenproblem
-      L L^T = D^1/2 (W^-1 - S-) D^1/2,   Sym = L^T D^1/2 (W^-1 - S+) D^1/2 L
-    (S+/- = even/odd Legendre parts of the phase matrix, D = W M^-1),
-    k^2 = eig(Sym), X = W^-1 D^1/2 L V, Y = -k W^-1 D^1/2 L^-T V
-  * layer operators  Q- = X m D-^-1, Q+ = Y m D+^-1,
-      D+ = X(1+e) - Y m,  D- = X m - Y(1+e),   R = Q- + Q+,  T = I - Q- + Q+
+      L L^T = D^1/2 (W^-1 - S-) D^1/2,   C C^T = D^1/2 (W^-1 - S+) D^1/2,
+      Sym = L^T C C^T L = B0^T B0 with B0 = C^T L;  the kernel's one-sided
+    Jacobi rotates B0's columns into B = B0 V, so k^2 = |b_j|^2 and
+    U = L V = C^-T B (here V comes from eigh of B0^T B0)
+  * layer operators in the flux-weighted basis, Omega = U Delta^1/2,
+    Psi^T = L^-T V Gamma^1/2, and by Woodbury
+      A- = (I + Omega Omega^T)^-1, A+ = (I + Psi^T Psi)^-1,
+      R~ = A+ - A-,  T~ = A- + A+ - I,  Q~- = I - A-,  Q~+ = A+ - I
   * sources from the beam/thermal particular solutions
   * adding sweep top->bottom (R_above, S_down), scalar Lambert surface,
     back-substitution bottom->top.
@@ -44,29 +47,33 @@ def layer_ops(dtau, ssa, chi, nstr, umu0, fbeam, b_top, b_bot, tauc_top):
     am = np.diag(1.0 / mu) - sd[:, None] * sminus * sd[None, :]
     ap = np.diag(1.0 / mu) - sd[:, None] * splus * sd[None, :]
     lch = np.linalg.cholesky(am)
-    sym = lch.T @ ap @ lch
-    k2, v = np.linalg.eigh(sym)
+    # one-sided Jacobi view (hd_layer_kernel): C C^T = -A+, B0 = C^T L, Sym = B0^T B0;
+    # the rotations give B = B0 V with k^2 = |b_j|^2, and U = L V = C^-T B
+    cch = np.linalg.cholesky(ap)
+    b0 = cch.T @ lch
+    k2, v = np.linalg.eigh(b0.T @ b0)
+    bcols = b0 @ v
+    k2 = np.sum(bcols * bcols, axis=0)
     k = np.sqrt(k2)
+    u = np.linalg.solve(cch.T, bcols)         # U = L V = C^-T B
     # ---- layer operators in the flux-weighted basis (g = sqrt(w mu)) ----
     e = np.exp(-k * taup)
     m = -np.expm1(-k * taup)
     th = m / (1.0 + e)                        # tanh(k tau'/2)
     delta = np.where(k * taup > 1e-8, th / np.where(k > 0, k, 1.0), 0.5 * taup)
     gamma = k * th
-    u = lch @ v                               # U = L V
     omega = u * np.sqrt(delta)[None, :]       # Omega = U Delta^1/2
-    psit = np.linalg.solve(lch.T, v) * np.sqrt(gamma)[None, :]   # Psi^T = L^-T V Gamma^1/2
-    hm = np.eye(nn) + omega.T @ omega
-    jm = np.linalg.cholesky(hm)
-    phi = np.linalg.solve(jm, omega.T).T      # Omega J^-T
-    qtm = phi @ phi.T                         # Q~- = Omega (I + Omega^T Omega)^-1 Omega^T
-    hp = np.eye(nn) + psit.T @ psit           # I + Psi Psi^T
-    jp = np.linalg.cholesky(hp)
-    xi = np.linalg.solve(jp, psit.T)          # J^-1 Psi
-    qtp = -(xi.T @ xi)                        # Q~+ = -Psi^T (I + Psi Psi^T)^-1 Psi
+    vv = np.linalg.solve(lch, u)              # V = L^-1 U
+    psit = np.linalg.solve(lch.T, vv) * np.sqrt(gamma)[None, :]   # Psi^T = L^-T V Gamma^1/2
+    # Woodbury: Q~- = I - A-, Q~+ = A+ - I with A- = (I + Omega Omega^T)^-1,
+    # A+ = (I + Psi^T Psi)^-1 (two SPD inverses from Cholesky factors)
+    aminus = np.linalg.inv(np.eye(nn) + omega @ omega.T)
+    aplus = np.linalg.inv(np.eye(nn) + psit @ psit.T)
+    qtm = np.eye(nn) - aminus
+    qtp = aplus - np.eye(nn)
     g = np.sqrt(w * mu)
-    rt = qtm + qtp                            # R~ (symmetric)
-    tt_ = np.eye(nn) - qtm + qtp              # T~ (symmetric)
+    rt = aplus - aminus                       # R~ (symmetric)
+    tt_ = aminus + aplus - np.eye(nn)         # T~ (symmetric)
 
     def linv(vec):   # W^-1 D^1/2 L^-T L^-1 D^1/2 vec
         z = np.linalg.solve(lch, sd * vec)
@@ -82,9 +89,9 @@ def layer_ops(dtau, ssa, chi, nstr, umu0, fbeam, b_top, b_bot, tauc_top):
         xs = fbeam / (2 * math.pi) * (pt[ev].T @ (gl[ev] * p0[ev]))
         xd = -fbeam / (2 * math.pi) * (pt[~ev].T @ (gl[~ev] * p0[~ev]))
         rv = -(1.0 / (mu * sd)) * (lch @ (lch.T @ (sd * xs))) + xd / (mu * umu0)
-        ttv = v.T @ np.linalg.solve(lch, (w / sd) * rv)
+        ttv = u.T @ np.linalg.solve(lch.T, np.linalg.solve(lch, (w / sd) * rv))   # V^T y2 = U^T L^-T y2
         ttv = ttv / (1.0 / umu0 ** 2 - k2)
-        svec = (sd / w) * (lch @ (v @ ttv))   # X tt, X = W^-1 D^1/2 L V
+        svec = (sd / w) * (u @ ttv)           # X tt, X = W^-1 D^1/2 L V = W^-1 D^1/2 U
         dd = linv(xd - mu * svec / umu0)
         att = math.exp(-tauc_top / umu0)
         zp = 0.5 * (svec + dd) * att
