@@ -421,9 +421,14 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_layer_kernel(LayerArgs A) 
 
   // ---- eigenpairs (c_soleig): Sym = L^T (-A+) L = V diag(k^2) V^T ----
   // With C C^T = -A+ (SPD because Sym is), Sym = B^T B for B = C^T L; the
-  // one-sided Jacobi on B's columns yields k^2 = |b_j|^2 and V.
-  double vt[NN];  // lane j: column j of V (row j of V^T)
-  double kk;      // lane j: k_j
+  // one-sided Jacobi on B's columns yields k^2 = |b_j|^2 and B = B0 V, so
+  // U = L V = C^-T B and V = L^-1 U.  Each of V, V^T y2 and U is consumed as
+  // soon as it exists (V rows -> Psi^T rows, then the beam, then U rows ->
+  // Omega rows), which keeps the live set to one team row-set at a time.
+  double kk;        // lane j: k_j
+  double pst[NN];   // lane i: row i of Psi^T = L^-T V Gamma^1/2
+  double omr[NN];   // lane i: row i of Omega = U Delta^1/2
+  double zp = 0.0, zm = 0.0, e0 = 0.0;
   {
     double unused[NN], rdc;
     if (!team_chol<NN, false>(ap, unused, rdc)) st |= kStEigen;  // ap <- rows of C
@@ -439,158 +444,134 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_layer_kernel(LayerArgs A) 
     sfor<0, NN>([&](auto K) { k2 = fma(bcol[HD_K(K)], bcol[HD_K(K)], k2); });
     if (act && !(k2 > 0.0)) st |= kStEigen;
     kk = sqrt(k2 > 0.0 ? k2 : 0.0) * msk;
-    // v_j = B0^-1 b_j = L^-1 C^-T b_j (lane-local solves, matrix entries broadcast)
+    // Delta = tanh(k tau'/2)/k, Gamma = k tanh(k tau'/2) (lane j)
+    double dsq, gsq;
+    {
+      const double x = kk * taup;
+      const double m = -expm1(-x);
+      const double th = m * rcp_nr(2.0 - m);
+      const double delta = x > 1.0e-8 ? th * rcp_nr(kk > 0.0 ? kk : 1.0) : 0.5 * taup;
+      dsq = sqrt(delta);
+      gsq = sqrt(kk * th);
+    }
+    // columns (lane j) of U = C^-T b_j and V = L^-1 U: lane-local solves with
+    // the matrix entries broadcast
     sfor_rev<0, NN>([&](auto I) {  // C^T y = b
       constexpr int r = HD_K(I);
       double t = bcol[r];
       sfor<r + 1, NN>([&](auto K) { t = fma(-bc<HD_K(K)>(ap[r]), bcol[HD_K(K)], t); });
-      bcol[r] = t * bc<r>(rdc);
+      bcol[r] = t * bc<r>(rdc) * msk;
     });
+    double vt[NN];  // lane j: column j of V (row j of V^T)
     sfor<0, NN>([&](auto I) {  // L x = y
       constexpr int r = HD_K(I);
       double t = bcol[r];
       sfor<0, r>([&](auto K) { t = fma(-bc<r>(lch[HD_K(K)]), vt[HD_K(K)], t); });
       vt[r] = t * bc<r>(rdl) * msk;
     });
-  }
-  // v = rows of V (lane i: V_ij over j): transpose through this team's LDS
-  // tile (a team lives in one wave and LDS operations of a wave complete in
-  // order, so no barrier; the row stride kTeam+1 keeps both passes conflict-free)
-  double v[NN];
-  {
+    // rows of V and U: transposes through this team's LDS tile (a team lives
+    // in one wave and LDS operations of a wave complete in order, so no
+    // barrier; the row stride kTeam+1 keeps both passes conflict-free)
     double* tile = tr_lds + (threadIdx.x >> 4) * (kTeam * (kTeam + 1));
     sfor<0, NN>([&](auto I) { tile[HD_K(I) * (kTeam + 1) + i] = vt[HD_K(I)]; });
     __builtin_amdgcn_wave_barrier();
-    sfor<0, NN>([&](auto J) { v[HD_K(J)] = tile[ii * (kTeam + 1) + HD_K(J)] * msk; });
+    sfor<0, NN>([&](auto J) {
+      pst[HD_K(J)] = tile[ii * (kTeam + 1) + HD_K(J)] * msk * bc<HD_K(J)>(gsq);
+    });
     __builtin_amdgcn_wave_barrier();
-  }
-
-  // ---- beam particular solution Z+/- (c_upbeam) ----
-  double zp = 0.0, zm = 0.0, e0 = 0.0;
-  if (beam) {
-    const double r2 = rmu0 * rmu0;
-    double t = 0.0;  // (V^T y2)_j
-    sfor<0, NN>([&](auto K) { t = fma(vt[HD_K(K)], bc<HD_K(K)>(y2), t); });
-    double den = fma(-kk, kk, r2);
-    if (act && fabs(den) < 1.0e-9 * r2) {
-      st |= kStResonance;
-      den = den < 0.0 ? -1.0e-9 * r2 : 1.0e-9 * r2;
+    team_umsolve<NN>(lt, rdl, pst);  // Psi^T rows = L^-T V Gamma^1/2
+    // ---- beam particular solution Z+/- (c_upbeam) ----
+    double tt = 0.0;  // lane j: (V^T y2)_j / (1/mu0^2 - k_j^2)
+    if (beam) {
+      const double r2 = rmu0 * rmu0;
+      double t = 0.0;
+      sfor<0, NN>([&](auto K) { t = fma(vt[HD_K(K)], bc<HD_K(K)>(y2), t); });
+      double den = fma(-kk, kk, r2);
+      if (act && fabs(den) < 1.0e-9 * r2) {
+        st |= kStResonance;
+        den = den < 0.0 ? -1.0e-9 * r2 : 1.0e-9 * r2;
+      }
+      tt = t / den * msk;
     }
-    const double tt = t / den * msk;
-    double y = 0.0;  // V tt
-    sfor<0, NN>([&](auto J) { y = fma(v[HD_K(J)], bc<HD_K(J)>(tt), y); });
-    double sv = 0.0;  // W^-1 D^1/2 L y
-    sfor<0, NN>([&](auto K) { sv = fma(lch[HD_K(K)], bc<HD_K(K)>(y), sv); });
-    sv *= rg_i;
-    double yy = sd_i * mu_i * sv;
-    team_lsolve<NN>(lch, rdl, yy);
-    team_usolve<NN>(lt, rdl, yy);
-    const double tauc = A.tauc[(size_t)lc * A.nsc + sl];
-    const double att = 0.5 * exp(-tauc * rmu0);
-    const double dd = rg_i * fma(-yy, rmu0, lxd);
-    zp = (sv + dd) * att;
-    zm = (sv - dd) * att;
-    e0 = exp(-taup * rmu0);
+    sfor<0, NN>([&](auto I) { tile[HD_K(I) * (kTeam + 1) + i] = bcol[HD_K(I)]; });
+    __builtin_amdgcn_wave_barrier();
+    double u[NN];  // lane i: row i of U
+    sfor<0, NN>([&](auto J) { u[HD_K(J)] = tile[ii * (kTeam + 1) + HD_K(J)] * msk; });
+    __builtin_amdgcn_wave_barrier();
+    if (beam) {
+      double sv = 0.0;  // W^-1 D^1/2 L V tt = W^-1 D^1/2 U tt
+      sfor<0, NN>([&](auto J) { sv = fma(u[HD_K(J)], bc<HD_K(J)>(tt), sv); });
+      sv *= rg_i;
+      double yy = sd_i * mu_i * sv;
+      team_lsolve<NN>(lch, rdl, yy);
+      team_usolve<NN>(lt, rdl, yy);
+      const double tauc = A.tauc[(size_t)lc * A.nsc + sl];
+      const double att = 0.5 * exp(-tauc * rmu0);
+      const double dd = rg_i * fma(-yy, rmu0, lxd);
+      zp = (sv + dd) * att;
+      zm = (sv - dd) * att;
+      e0 = exp(-taup * rmu0);
+    }
+    // ---- layer operators in the flux-weighted basis: Omega rows ----
+    sfor<0, NN>([&](auto J) { omr[HD_K(J)] = u[HD_K(J)] * bc<HD_K(J)>(dsq); });
   }
-
-  // ---- layer operators in the flux-weighted basis ----
-  double dsq, gsq;
-  {
-    const double x = kk * taup;
-    const double m = -expm1(-x);
-    const double th = m * rcp_nr(2.0 - m);
-    const double delta = x > 1.0e-8 ? th * rcp_nr(kk > 0.0 ? kk : 1.0) : 0.5 * taup;
-    dsq = sqrt(delta);
-    gsq = sqrt(kk * th);
-  }
-  // Psi^T rows = L^-T V Gamma^1/2
-  double pst[NN];
-  sfor<0, NN>([&](auto J) { pst[HD_K(J)] = v[HD_K(J)] * bc<HD_K(J)>(gsq); });
-  team_umsolve<NN>(lt, rdl, pst);
-  // Omega rows = L V Delta^1/2
-  double omr[NN];
-  sfor<0, NN>([&](auto J) {
-    constexpr int j = HD_K(J);
-    double t = 0.0;
-    sfor<0, NN>([&](auto K) { t = fma(lch[HD_K(K)], bc<HD_K(K)>(v[j]), t); });
-    omr[j] = t * bc<j>(dsq);
-  });
-  // Omega^T rows (lane j): dsq_j sum_a V_aj L_ca
-  double omt[NN];
-  sfor<0, NN>([&](auto C) {
-    constexpr int c = HD_K(C);
-    double t = 0.0;
-    sfor<0, c + 1>([&](auto K) { t = fma(vt[HD_K(K)], bc<c>(lch[HD_K(K)]), t); });
-    omt[c] = t * dsq;
-  });
-  // Psi rows (lane j): gsq_j (V^T)_j L^-1, i.e. x L = vt_j by backward columns
-  double psr[NN];
-  sfor_rev<0, NN>([&](auto C) {
-    constexpr int c = HD_K(C);
-    double t = vt[c];
-    sfor<c + 1, NN>([&](auto K) { t = fma(-psr[HD_K(K)], bc<HD_K(K)>(lch[c]), t); });
-    psr[c] = t * bc<c>(rdl);
-  });
-  sfor<0, NN>([&](auto J) { psr[HD_K(J)] *= gsq; });
-
   const double ga = g_i * (cvec - fma(-zp, e0, zm));
   const double gb = g_i * (fma(zp, e0, zm) + bsum);
-  // Q~- = Phi Phi^T, Phi = Omega J^-T, J J^T = I + Omega^T Omega
-  double qm[NN], pv = 0.0;
+  // By Woodbury, Q~- = I - A- and Q~+ = A+ - I with A- = (I + Omega Omega^T)^-1,
+  // A+ = (I + Psi^T Psi)^-1 (SPD, eigenvalues in (0, 1]); lane i gets row i of
+  // each inverse from the Cholesky rows J by two lane-local triangular solves
+  // with broadcast J entries:  z J^T = e_i, then a J = z  (a = e_i (J J^T)^-1).
+  double am_[NN], ap_[NN];
+  auto spd_inverse_row = [&](double (&h)[NN], double (&arow)[NN]) {
+    double unused[NN], jrd;
+    if (!team_chol<NN, false>(h, unused, jrd)) st |= kStEigen;  // h <- row i of J
+    double z[NN];
+    sfor<0, NN>([&](auto R) {
+      constexpr int r = HD_K(R);
+      double t = i == r ? 1.0 : 0.0;
+      sfor<0, r>([&](auto K) { t = fma(-bc<r>(h[HD_K(K)]), z[HD_K(K)], t); });
+      z[r] = t * bc<r>(jrd);
+    });
+    // both solves broadcast the same J entries; without this the compiler
+    // would keep all NN(NN-1)/2 broadcast values live from one solve to the next
+#pragma unroll
+    for (int k = 0; k < NN; ++k) asm volatile("" : "+v"(h[k]));
+    asm volatile("" : "+v"(jrd));
+    sfor_rev<0, NN>([&](auto C) {
+      constexpr int c = HD_K(C);
+      double t = z[c];
+      sfor<c + 1, NN>([&](auto K) { t = fma(-arow[HD_K(K)], bc<HD_K(K)>(h[c]), t); });
+      arow[c] = t * bc<c>(jrd);
+    });
+  };
   {
-    double hm[NN];
+    double hm[NN];  // row i of I + Omega Omega^T
     sfor<0, NN>([&](auto J) {
       constexpr int j = HD_K(J);
       double t = i == j ? 1.0 : 0.0;
-      sfor<0, NN>([&](auto K) { t = fma(omt[HD_K(K)], bc<HD_K(K)>(omr[j]), t); });
+      sfor<0, NN>([&](auto K) { t = fma(omr[HD_K(K)], bc<j>(omr[HD_K(K)]), t); });
       hm[j] = t;
     });
-    double unused[NN], jrd;
-    if (!team_chol<NN, false>(hm, unused, jrd)) st |= kStEigen;
-    double ph[NN];
-    sfor<0, NN>([&](auto J) {
-      constexpr int j = HD_K(J);
-      double t = omr[j];
-      sfor<0, j>([&](auto K) { t = fma(-bc<j>(hm[HD_K(K)]), ph[HD_K(K)], t); });
-      ph[j] = t * bc<j>(jrd);
-    });
-    sfor<0, NN>([&](auto J) {
-      constexpr int j = HD_K(J);
-      double t = 0.0;
-      sfor<0, NN>([&](auto K) { t = fma(ph[HD_K(K)], bc<j>(ph[HD_K(K)]), t); });
-      qm[j] = t;
-      pv = fma(t, bc<j>(ga), pv);
-    });
+    spd_inverse_row(hm, am_);
   }
-  // Q~+ = -Xi^T Xi, Xi^T rows = Psi^T rows through J+, J+ J+^T = I + Psi Psi^T
-  double qp[NN], qv = 0.0;
   {
-    double hp[NN];
+    double hp[NN];  // row i of I + Psi^T Psi
     sfor<0, NN>([&](auto J) {
       constexpr int j = HD_K(J);
       double t = i == j ? 1.0 : 0.0;
-      sfor<0, NN>([&](auto K) { t = fma(psr[HD_K(K)], bc<j>(psr[HD_K(K)]), t); });
+      sfor<0, NN>([&](auto K) { t = fma(pst[HD_K(K)], bc<j>(pst[HD_K(K)]), t); });
       hp[j] = t;
     });
-    double unused[NN], jrd;
-    if (!team_chol<NN, false>(hp, unused, jrd)) st |= kStEigen;
-    double xi[NN];
-    sfor<0, NN>([&](auto J) {
-      constexpr int j = HD_K(J);
-      double t = pst[j];
-      sfor<0, j>([&](auto K) { t = fma(-bc<j>(hp[HD_K(K)]), xi[HD_K(K)], t); });
-      xi[j] = t * bc<j>(jrd);
-    });
-    sfor<0, NN>([&](auto J) {
-      constexpr int j = HD_K(J);
-      double t = 0.0;
-      sfor<0, NN>([&](auto K) { t = fma(xi[HD_K(K)], bc<j>(xi[HD_K(K)]), t); });
-      qp[j] = -t;
-      qv = fma(-t, bc<j>(gb), qv);
-    });
+    spd_inverse_row(hp, ap_);
   }
+  double pv = ga, qv = -gb;  // Q~- ga = ga - A- ga,  Q~+ gb = A+ gb - gb
+  sfor<0, NN>([&](auto J) {
+    constexpr int j = HD_K(J);
+    pv = fma(-am_[j], bc<j>(ga), pv);
+    qv = fma(ap_[j], bc<j>(gb), qv);
+  });
 
-  // ---- store: R~ = Q~- + Q~+, T~ = I - Q~- + Q~+ (rows), S~+, S~-, tau' ----
+  // ---- store: R~ = A+ - A-, T~ = A- + A+ - I (rows), S~+, S~-, tau' ----
   // lanes >= NN store into a sink instead of branching around the stores (a
   // branch here costs the whole kernel's register allocation at NN < 16)
   double* rec = A.scr + ((size_t)lc * A.nsc + sl) * ne1t<NN>();
@@ -598,8 +579,8 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_layer_kernel(LayerArgs A) 
   double chk = 0.0;
   sfor<0, NN>([&](auto J) {
     constexpr int j = HD_K(J);
-    const double r = qm[j] + qp[j];
-    const double t = (i == j ? 1.0 : 0.0) - qm[j] + qp[j];
+    const double r = ap_[j] - am_[j];
+    const double t = (am_[j] + ap_[j]) - (i == j ? 1.0 : 0.0);
     out[ii * NN + j] = r;
     out[NN * NN + ii * NN + j] = t;
     chk += r + t;
