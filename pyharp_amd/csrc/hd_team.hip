@@ -226,12 +226,16 @@ __host__ __device__ constexpr bool round_has_pair(int m) {
 // eigenvectors come out afterwards as V = B0^-1 B (two triangular solves, see
 // the layer kernel), which removes half of the cross-lane traffic per round.
 constexpr double kJacobiTol2 = 1.0e-30;  // rotate while (b_p.b_q)^2 > tol |b_p|^2 |b_q|^2
-constexpr double kJacobiLast2 = 1.0e-18;  // a sweep whose largest such ratio stayed below
-                                          // this leaves ~1e-18^2: the last one needed
+// the last sweep needed: the one whose off-diagonal Frobenius norm of B^T B
+// (accumulated from the pairs' b_p.b_q as they were rotated) stayed below 1e-8
+// of its diagonal -- quadratic convergence leaves ~1e-16 after it (the register
+// path's jacobi_os rule; at nstr = 32 one sweep fewer than a per-pair 1e-9 cosine
+// bound for the same residual, ~4e-15)
+constexpr double kJacobiLastFrob2 = 1.0e-16;
 
 template <int NN, int M>
 __device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double& own, bool on,
-                                                  bool& big) {
+                                                  double& off) {
   const int i = tlane();
   const int pi = i ^ M;
   double bq[NN];
@@ -250,7 +254,7 @@ __device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double& own, 
   const bool pair = i < NN && pi < NN;
   const double g2 = gam * gam, pq = app * aqq;
   const bool r = on && pair && g2 > kJacobiTol2 * pq;
-  big = big || (pair && g2 > kJacobiLast2 * pq);
+  off += pair ? g2 : 0.0;  // each pair counted by both of its lanes
   // w = sqrt(d^2 + 4 g^2), u = |d| + w, z = 1/sqrt(2 w u): c = u z, s = sgn(d) 2 g z
   const double d = aqq - app;
   const double w2 = r ? fma(d, d, 4.0 * g2) : 1.0;
@@ -267,22 +271,23 @@ __device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double& own, 
   own = lo ? fma(cc, app, fma(ss2, aqq, -cs2)) : fma(ss2, app, fma(cc, aqq, cs2));
 }
 
-// Sweeps of rounds 1..15 until a sweep's largest rotation was small enough
-// that it was the last one needed (quadratic convergence), or max_sweeps.
-// A converged team issues no-op rotations while its wave-mates finish.
+// Sweeps of rounds 1..15 until the sweep that was the last one needed
+// (kJacobiLastFrob2), or max_sweeps.  A converged team issues no-op rotations
+// (c = 1, s = 0) while its wave-mates finish.
 template <int NN>
 __device__ __forceinline__ void team_jacobi(double (&b)[NN], int max_sweeps) {
   bool on = true;
   for (int sweep = 0; sweep < max_sweeps; ++sweep) {
-    bool big = false;  // some pair of this lane had (b_p.b_q)^2 > kJacobiLast2 |b_p|^2 |b_q|^2
+    double off = 0.0;  // this lane's sum of (b_p.b_q)^2 over its pairs in this sweep
     double own = 0.0;  // |b_j|^2, exact at the start of every sweep, then tracked
     sfor<0, NN>([&](auto K) { own = fma(b[HD_K(K)], b[HD_K(K)], own); });
+    const double dia = bc<0>(team_sum(own * own));  // sum_j |b_j|^4 (team-uniform)
     sfor<1, kTeam>([&](auto Mc) {
       constexpr int m = HD_K(Mc);
-      if constexpr (round_has_pair<NN>(m)) team_jacobi_round<NN, m>(b, own, on, big);
+      if constexpr (round_has_pair<NN>(m)) team_jacobi_round<NN, m>(b, own, on, off);
     });
-    // team max via the sum of indicator flags (uniform over the team)
-    on = bc<0>(team_sum(big ? 1.0 : 0.0)) > 0.0;
+    // every pair was counted twice (once per lane): compare 2x the bound
+    on = on && bc<0>(team_sum(off)) > 2.0 * kJacobiLastFrob2 * dia;
     if (__all(!on)) break;
   }
 }
