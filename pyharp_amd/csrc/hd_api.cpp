@@ -505,7 +505,7 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
         HD_HIP(ctx, hipEventRecord(ctx->ev_pro[buf ^ 1], ctx->side));
       }
       HD_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_sweep[buf], 0));
-      e = hd::launch_backsub_nn(nn, sa, ctx->side);
+      e = hd::launch_backsub_nn(nn, sa, ctx->side, s1 >= nsolve);  // last chunk: tail kernel
       if (e != hipSuccess)
         return fail(ctx, HD_EHIP, "hd_solve: back-substitution launch failed: %s",
                     hipGetErrorString(e));

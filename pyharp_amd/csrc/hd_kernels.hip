@@ -749,9 +749,11 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
 // sweep's register file allows one wave per SIMD): a pure stream over the
 // back-substitution records, I+_top = t + ZT I+_bottom, fluxes per level.
 // ============================================================================
-template <int NN>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
-void hd_backsub_kernel(SweepArgs A) {
+// The arithmetic of both back-substitution kernels (identical expression order,
+// so a solve's fluxes do not depend on which kernel ran its chunk).  PRE: the
+// next layer's record is loaded into registers before this layer is computed.
+template <int NN, bool PRE>
+__device__ __forceinline__ void backsub_body(const SweepArgs& A) {
   const Quad<NN>& Qc = quad<NN>();
   const long sl = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (sl >= A.nsc) return;
@@ -765,32 +767,79 @@ void hd_backsub_kernel(SweepArgs A) {
   for (int i = 0; i < NN; ++i) ip[i] = Qc.g[i] * x;
   double* fo = A.flux + (size_t)s * (L + 1) * 2;
   double chk = 0.0;
-  for (int lc = L - 1; lc >= 0; --lc) {
-    const double* bp = A.bsub + (size_t)lc * ne2<NN>() * nsc + sl;
+  // element e of this layer's record (e = i NN + j: ZT; NN^2 + i: t;
+  // NN^2 + NN + i: rc; NN^2 + 2 NN: cs) through `get`
+  auto layer = [&](int lc, auto&& get) {
     double nip[NN];
 #pragma unroll
     for (int i = 0; i < NN; ++i) {
-      double t = bp[(NN * NN + i) * nsc];
+      double t = get(NN * NN + i);
 #pragma unroll
-      for (int j = 0; j < NN; ++j) t += bp[(i * NN + j) * nsc] * ip[j];
+      for (int j = 0; j < NN; ++j) t += get(i * NN + j) * ip[j];
       nip[i] = t;
     }
-    double up = 0.0, dn = bp[(NN * NN + 2 * NN) * nsc];
+    double up = 0.0, dn = get(NN * NN + 2 * NN);
 #pragma unroll
     for (int i = 0; i < NN; ++i) {
       ip[i] = nip[i];
       up += Qc.g[i] * nip[i];
-      dn += bp[(NN * NN + NN + i) * nsc] * nip[i];
+      dn += get(NN * NN + NN + i) * nip[i];
     }
     const int lev = L - lc;
     fo[2 * lev] = twopi * up;
     fo[2 * lev + 1] = dn;
     chk += fo[2 * lev] + fo[2 * lev + 1];
+  };
+  auto rec_ptr = [&](int lc) { return A.bsub + (size_t)lc * ne2<NN>() * nsc + sl; };
+  if constexpr (PRE) {
+    constexpr int NE = NN * NN + 2 * NN + 1;
+    double cur[NE], nxt[NE];
+    {
+      const double* bp = rec_ptr(L - 1);
+#pragma unroll
+      for (int e = 0; e < NE; ++e) cur[e] = bp[e * nsc];
+    }
+    for (int lc = L - 1; lc >= 0; --lc) {
+      if (lc > 0) {
+        const double* bp = rec_ptr(lc - 1);
+#pragma unroll
+        for (int e = 0; e < NE; ++e) nxt[e] = bp[e * nsc];
+      }
+      layer(lc, [&](int e) { return cur[e]; });
+#pragma unroll
+      for (int e = 0; e < NE; ++e) cur[e] = nxt[e];
+    }
+  } else {
+    for (int lc = L - 1; lc >= 0; --lc) {
+      const double* bp = rec_ptr(lc);
+      layer(lc, [&](int e) { return bp[e * nsc]; });
+    }
   }
   if (!isfinite(chk)) {
     atomicOr(&A.status[s], kStNonFinite);
     atomicOr(A.anyerr, 1);
   }
+}
+
+// K3: per-solve back-substitution bottom -> top.  Split from the adding sweep
+// so that it runs at the occupancy of its own small register footprint (the
+// sweep's register file allows one wave per SIMD): a pure stream over the
+// back-substitution records, I+_top = t + ZT I+_bottom, fluxes per level.
+// This one runs on the side stream beside the next chunk's layer kernel, so it
+// must stay small (44 VGPRs: one wave fits next to a layer-kernel wave).
+template <int NN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
+void hd_backsub_kernel(SweepArgs A) {
+  backsub_body<NN, false>(A);
+}
+
+// K3 for the last chunk of a call, which nothing overlaps: no occupancy cap,
+// a whole layer record in flight at once and the next one loaded while this
+// one is computed (the capped kernel issues the 81 loads of a layer in small
+// register-limited batches, each waiting out a memory latency).
+template <int NN>
+__global__ __launch_bounds__(64) void hd_backsub_tail_kernel(SweepArgs A) {
+  backsub_body<NN, true>(A);
 }
 
 // ============================================================================
@@ -850,21 +899,25 @@ static hipError_t launch_chunk(const PlanckArgs* pa, const TaucArgs* ta, const L
 }
 
 template <int NN>
-static void launch_backsub(const SweepArgs& sa, hipStream_t stream) {
-  hipLaunchKernelGGL(hd_backsub_kernel<NN>, dim3((unsigned)((sa.nsc + 255) / 256)), dim3(256), 0,
-                     stream, sa);
+static void launch_backsub(const SweepArgs& sa, hipStream_t stream, bool tail) {
+  if (tail)
+    hipLaunchKernelGGL(hd_backsub_tail_kernel<NN>, dim3((unsigned)((sa.nsc + 63) / 64)), dim3(64),
+                       0, stream, sa);
+  else
+    hipLaunchKernelGGL(hd_backsub_kernel<NN>, dim3((unsigned)((sa.nsc + 255) / 256)), dim3(256),
+                       0, stream, sa);
 }
 
-hipError_t launch_backsub_nn(int nn, const SweepArgs& sa, hipStream_t stream) {
+hipError_t launch_backsub_nn(int nn, const SweepArgs& sa, hipStream_t stream, bool tail) {
   switch (nn) {
-    case 1: launch_backsub<1>(sa, stream); break;
-    case 2: launch_backsub<2>(sa, stream); break;
-    case 3: launch_backsub<3>(sa, stream); break;
-    case 4: launch_backsub<4>(sa, stream); break;
-    case 5: launch_backsub<5>(sa, stream); break;
-    case 6: launch_backsub<6>(sa, stream); break;
-    case 7: launch_backsub<7>(sa, stream); break;
-    case 8: launch_backsub<8>(sa, stream); break;
+    case 1: launch_backsub<1>(sa, stream, tail); break;
+    case 2: launch_backsub<2>(sa, stream, tail); break;
+    case 3: launch_backsub<3>(sa, stream, tail); break;
+    case 4: launch_backsub<4>(sa, stream, tail); break;
+    case 5: launch_backsub<5>(sa, stream, tail); break;
+    case 6: launch_backsub<6>(sa, stream, tail); break;
+    case 7: launch_backsub<7>(sa, stream, tail); break;
+    case 8: launch_backsub<8>(sa, stream, tail); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
