@@ -319,6 +319,7 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
       lxd[i] = Qc.sd[i] * xdi;
     }
     lower_solve<NN>(lch, rdl, y2);
+    lower_t_solve<NN>(lch, rdl, y2);  // L^-T y2: V^T y2 = U^T L^-T y2 below
     lower_solve<NN>(lch, rdl, lxd);
     lower_t_solve<NN>(lch, rdl, lxd);
   } else {
@@ -364,39 +365,41 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
       for (int k = 0; k <= i; ++k) rr[(e++) * nu] = lch[i][k];
   }
 
-  double sym[NN][NN];
+  // ---- eigenpairs (hd_layer_kernel's form): C C^T = -A+, Sym = B^T B for
+  // B = C^T L; the one-sided Jacobi gives k^2 = |b_j|^2 and B = B0 V, so
+  // U = L V = C^-T B; V = L^-1 U is stored for the later kernels ----
+  double rdc[NN];
+  if (!chol_inplace<NN>(ap, rdc)) st |= kStEigen;  // lower ap <- C
+  double v[NN][NN];  // B, then U = L V, then Omega = U Delta^1/2
 #pragma unroll
-  for (int j = 0; j < NN; ++j) {
-    double mcol[NN];
+  for (int i = 0; i < NN; ++i)
 #pragma unroll
-    for (int i = 0; i < NN; ++i) {
+    for (int j = 0; j < NN; ++j) {  // B_ij = sum_{k >= max(i,j)} C_ki L_kj
       double t = 0.0;
 #pragma unroll
-      for (int k = j; k < NN; ++k) t = fma(HD_SYM(ap, i, k), lch[k][j], t);
-      mcol[i] = t;
+      for (int k = (i > j ? i : j); k < NN; ++k) t = fma(ap[k][i], lch[k][j], t);
+      v[i][j] = t;
     }
-#pragma unroll
-    for (int i = 0; i <= j; ++i) {
-      double t = 0.0;
-#pragma unroll
-      for (int k = i; k < NN; ++k) t = fma(lch[k][i], mcol[k], t);
-      sym[i][j] = t;
-    }
-  }
-  double v[NN][NN];
-  jacobi_eig<NN>(sym, v, A.max_sweeps);
+  jacobi_os<NN>(v, A.max_sweeps);
   double kk[NN];
 #pragma unroll
   for (int j = 0; j < NN; ++j) {
-    const double k2 = sym[j][j];
+    double k2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < NN; ++i) k2 = fma(v[i][j], v[i][j], k2);
     if (!(k2 > 0.0)) st |= kStEigen;
     kk[j] = sqrt(k2 > 0.0 ? k2 : 0.0);
     rr[(oK + j) * nu] = kk[j];
   }
 #pragma unroll
-  for (int i = 0; i < NN; ++i)
+  for (int j = 0; j < NN; ++j) {  // U = C^-T B, column by column
+    double x[NN];
 #pragma unroll
-    for (int j = 0; j < NN; ++j) rr[(oV + i * NN + j) * nu] = v[i][j];
+    for (int i = 0; i < NN; ++i) x[i] = v[i][j];
+    lower_t_solve<NN>(ap, rdc, x);
+#pragma unroll
+    for (int i = 0; i < NN; ++i) v[i][j] = x[i];
+  }
 
   // ---- beam particular solution at the layer top ----
   double zp[NN], zm[NN];
@@ -405,7 +408,7 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
     double tt[NN];
     const double r2 = rmu0 * rmu0;
 #pragma unroll
-    for (int j = 0; j < NN; ++j) {
+    for (int j = 0; j < NN; ++j) {  // tt = V^T y2 / (1/mu0^2 - k^2), V^T y2 = U^T (L^-T y2)
       double t = 0.0;
 #pragma unroll
       for (int i = 0; i < NN; ++i) t = fma(v[i][j], y2[i], t);
@@ -418,17 +421,10 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
     }
     double sv[NN], y[NN];
 #pragma unroll
-    for (int i = 0; i < NN; ++i) {
+    for (int i = 0; i < NN; ++i) {  // s = W^-1 D^1/2 L V tt = W^-1 D^1/2 U tt
       double t = 0.0;
 #pragma unroll
       for (int j = 0; j < NN; ++j) t = fma(v[i][j], tt[j], t);
-      y[i] = t;
-    }
-#pragma unroll
-    for (int i = 0; i < NN; ++i) {
-      double t = 0.0;
-#pragma unroll
-      for (int k = 0; k <= i; ++k) t = fma(lch[i][k], y[k], t);
       sv[i] = Qc.rg[i] * t;
     }
 #pragma unroll
@@ -468,23 +464,21 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
   }
   rr[oE0 * nu] = e0;
 #pragma unroll
-  for (int j = 0; j < NN; ++j) {
+  for (int j = 0; j < NN; ++j) {  // V = L^-1 U (stored), Psi^T = L^-T V Gamma^1/2 -> LDS
     double x[NN];
 #pragma unroll
     for (int i = 0; i < NN; ++i) x[i] = v[i][j];
+    lower_solve<NN>(lch, rdl, x);
+#pragma unroll
+    for (int i = 0; i < NN; ++i) rr[(oV + i * NN + j) * nu] = x[i];
     lower_t_solve<NN>(lch, rdl, x);
 #pragma unroll
     for (int i = 0; i < NN; ++i) psi_lds[(i * NN + j) * kLayerBlockR + lt] = x[i] * gsq[j];
   }
 #pragma unroll
-  for (int i = NN - 1; i >= 0; --i)
+  for (int i = 0; i < NN; ++i)  // Omega = L V Delta^1/2 = U Delta^1/2
 #pragma unroll
-    for (int j = 0; j < NN; ++j) {
-      double t = 0.0;
-#pragma unroll
-      for (int a = 0; a <= i; ++a) t = fma(lch[i][a], v[a][j], t);
-      v[i][j] = t * dsq[j];
-    }
+    for (int j = 0; j < NN; ++j) v[i][j] *= dsq[j];
 
   double* out = A.rsw + (size_t)lc * ne1<NN>() * nu + u;
   double ga[NN], gb[NN];
@@ -493,72 +487,56 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
     ga[i] = Qc.g[i] * (cvec[i] - fma(-zp[i], e0, zm[i]));
     gb[i] = Qc.g[i] * (fma(zp[i], e0, zm[i]) + bsum);
   }
-  double pvec[NN], qmr[NN][NN];
+  // Woodbury (as hd_layer_kernel): Q~- = I - A-, Q~+ = A+ - I with
+  // A- = (I + Omega Omega^T)^-1, A+ = (I + Psi^T Psi)^-1; R~ = A+ - A-, T~ = A- + A+ - I
+  double pvec[NN], am_[NN][NN];
   {
-    double hm[NN][NN], rdh[NN];
 #pragma unroll
     for (int i = 0; i < NN; ++i)
 #pragma unroll
       for (int j = i; j < NN; ++j) {
         double t = (i == j) ? 1.0 : 0.0;
 #pragma unroll
-        for (int k = 0; k < NN; ++k) t = fma(v[k][i], v[k][j], t);
-        hm[i][j] = t;
-      }
-    if (!chol_inplace<NN>(hm, rdh)) st |= kStEigen;
-#pragma unroll
-    for (int r = 0; r < NN; ++r) lower_solve<NN>(hm, rdh, v[r]);
-#pragma unroll
-    for (int i = 0; i < NN; ++i) pvec[i] = 0.0;
-#pragma unroll
-    for (int i = 0; i < NN; ++i)
-#pragma unroll
-      for (int j = i; j < NN; ++j) {
-        double t = 0.0;
-#pragma unroll
         for (int k = 0; k < NN; ++k) t = fma(v[i][k], v[j][k], t);
-        qmr[i][j] = t;
-        pvec[i] = fma(t, ga[j], pvec[i]);
-        if (j != i) pvec[j] = fma(t, ga[i], pvec[j]);
+        am_[i][j] = t;
       }
+    double rdh[NN];
+    if (!chol_inplace<NN>(am_, rdh)) st |= kStEigen;
+    spd_inverse_upper<NN>(am_, rdh);
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {  // p = Q~- ga = ga - A- ga
+      double t = ga[i];
+#pragma unroll
+      for (int j = 0; j < NN; ++j) t = fma(-HD_SYM(am_, i, j), ga[j], t);
+      pvec[i] = t;
+    }
   }
-  double qp[NN][NN];
+  double ap_[NN][NN], qvec[NN];
   {
-    double pt_[NN][NN];
+    double pt_[NN][NN];  // pt_[i][j] = Psi^T[i][j]
 #pragma unroll
     for (int i = 0; i < NN; ++i)
 #pragma unroll
       for (int j = 0; j < NN; ++j) pt_[i][j] = psi_lds[(i * NN + j) * kLayerBlockR + lt];
-    double hp[NN][NN], rdh[NN];
 #pragma unroll
     for (int i = 0; i < NN; ++i)
 #pragma unroll
       for (int j = i; j < NN; ++j) {
         double t = (i == j) ? 1.0 : 0.0;
 #pragma unroll
-        for (int k = 0; k < NN; ++k) t = fma(pt_[k][i], pt_[k][j], t);
-        hp[i][j] = t;
-      }
-    if (!chol_inplace<NN>(hp, rdh)) st |= kStEigen;
-#pragma unroll
-    for (int r = 0; r < NN; ++r) lower_solve<NN>(hp, rdh, pt_[r]);
-#pragma unroll
-    for (int i = 0; i < NN; ++i)
-#pragma unroll
-      for (int j = i; j < NN; ++j) {
-        double t = 0.0;
-#pragma unroll
         for (int k = 0; k < NN; ++k) t = fma(pt_[i][k], pt_[j][k], t);
-        qp[i][j] = -t;
+        ap_[i][j] = t;
       }
-  }
-  double qvec[NN];
+    double rdh[NN];
+    if (!chol_inplace<NN>(ap_, rdh)) st |= kStEigen;
+    spd_inverse_upper<NN>(ap_, rdh);
 #pragma unroll
-  for (int i = 0; i < NN; ++i) {
-    double t = 0.0;
+    for (int i = 0; i < NN; ++i) {  // q = Q~+ gb = A+ gb - gb
+      double t = -gb[i];
 #pragma unroll
-    for (int j = 0; j < NN; ++j) t = fma(HD_SYM(qp, i, j), gb[j], t);
-    qvec[i] = t;
+      for (int j = 0; j < NN; ++j) t = fma(HD_SYM(ap_, i, j), gb[j], t);
+      qvec[i] = t;
+    }
   }
   double chk = 0.0;
   {
@@ -567,9 +545,8 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
     for (int i = 0; i < NN; ++i)
 #pragma unroll
       for (int j = i; j < NN; ++j) {
-        const double qm = qmr[i][j];
-        const double r = qm + qp[i][j];
-        const double t = ((i == j) ? 1.0 : 0.0) - qm + qp[i][j];
+        const double r = ap_[i][j] - am_[i][j];
+        const double t = (am_[i][j] + ap_[i][j]) - ((i == j) ? 1.0 : 0.0);
         out[e * nu] = r;
         out[(nsym + e) * nu] = t;
         chk += r + t;
