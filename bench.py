@@ -351,7 +351,11 @@ def main():
                     "avg_launch_ms": round(k1_avg_ms, 3),
                     "flop_per_solve": k1_flop,
                     "note": "FP64 compute bound (gfx950 FP64 vector and MFMA peaks are equal); "
-                            "achieved uses the SURVEY 8(d) algorithmic FLOP convention"}
+                            "achieved uses the SURVEY 8(d) algorithmic FLOP convention"
+                            + ("; nstr<=16: each launch runs on its own stream beside the "
+                               "previous chunk's sweep, so its duration includes that "
+                               "co-running (path_roofline is what the throughput follows)"
+                               if nstr <= 16 else "")}
         whole = {"achieved_tflops": round(total_flop * value / 1e12, 3),
                  "frac": round(total_flop * value / 1e12 / FP64_PEAK_TFLOPS / world, 4),
                  "layer_ms_per_step": round(tm.layer_ms / steps_timed, 3),

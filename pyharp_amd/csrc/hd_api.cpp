@@ -39,6 +39,10 @@ struct hd_context {
   // register path: back-substitution of chunk k on `side`, beside chunk k+1's
   // layer kernel (its 44-VGPR waves fit next to the layer kernel's on a SIMD)
   hipStream_t side = nullptr;
+  // register path: chunk k+1's layer kernel on its own stream, beside chunk k's
+  // sweep (it takes the SIMDs a partial sweep leaves idle)
+  hipStream_t lay = nullptr;
+  hipEvent_t ev_layer[2] = {nullptr, nullptr};
   hipEvent_t ev_sweep[2] = {nullptr, nullptr};
   hipEvent_t ev_back[2] = {nullptr, nullptr};
   hipEvent_t ev_pro[2] = {nullptr, nullptr};  // next chunk's prologue done (side stream)
@@ -183,13 +187,13 @@ int ensure_status(hd_context* ctx, size_t n) {
   return HD_OK;
 }
 
-// fold every recorded (K1 start, K1 end = K2 start, K2 end) triple into the totals
+// fold every recorded (K1 start, K1 end, K2 start, K2 end) quadruple into the totals
 int resolve_timing(hd_context* ctx) {
-  for (size_t i = 0; i + 3 <= ctx->pool_used; i += 3) {
-    HD_HIP(ctx, hipEventSynchronize(ctx->pool[i + 2]));
+  for (size_t i = 0; i + 4 <= ctx->pool_used; i += 4) {
+    HD_HIP(ctx, hipEventSynchronize(ctx->pool[i + 3]));
     float t1 = 0.f, t2 = 0.f;
     HD_HIP(ctx, hipEventElapsedTime(&t1, ctx->pool[i], ctx->pool[i + 1]));
-    HD_HIP(ctx, hipEventElapsedTime(&t2, ctx->pool[i + 1], ctx->pool[i + 2]));
+    HD_HIP(ctx, hipEventElapsedTime(&t2, ctx->pool[i + 2], ctx->pool[i + 3]));
     ctx->times.layer_ms += t1;
     ctx->times.sweep_ms += t2;
     ctx->times.layer_launches += 1;
@@ -263,9 +267,11 @@ int hd_context_create(hd_context** out, int device) {
   HD_HIP(ctx, hipSetDevice(device));
   HD_HIP(ctx, hipMalloc(&ctx->anyerr, sizeof(int)));
   HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+  HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->lay, hipStreamNonBlocking));
   HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
   HD_HIP(ctx, hipMalloc(&ctx->sink, 4096 * sizeof(double)));
   for (int b = 0; b < 2; ++b) {
+    HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_layer[b], hipEventDisableTiming));
     HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_sweep[b], hipEventDisableTiming));
     HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_back[b], hipEventDisableTiming));
     HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_pro[b], hipEventDisableTiming));
@@ -281,6 +287,7 @@ int hd_context_destroy(hd_context* ctx) {
   if (ctx->status) (void)hipFree(ctx->status);
   if (ctx->anyerr) (void)hipFree(ctx->anyerr);
   for (int b = 0; b < 2; ++b) {
+    if (ctx->ev_layer[b]) (void)hipEventDestroy(ctx->ev_layer[b]);
     if (ctx->ev_sweep[b]) (void)hipEventDestroy(ctx->ev_sweep[b]);
     if (ctx->ev_back[b]) (void)hipEventDestroy(ctx->ev_back[b]);
     if (ctx->ev_pro[b]) (void)hipEventDestroy(ctx->ev_pro[b]);
@@ -289,6 +296,7 @@ int hd_context_destroy(hd_context* ctx) {
   if (ctx->sink) (void)hipFree(ctx->sink);
   if (ctx->rad_grid) (void)hipFree(ctx->rad_grid);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
+  if (ctx->lay) (void)hipStreamDestroy(ctx->lay);
   for (auto& e : ctx->pool)
     if (e) (void)hipEventDestroy(e);
   delete ctx;
@@ -378,16 +386,19 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
   const int nb = reg ? 2 : 1;  // buffers of the per-chunk regions that live across chunks
   // Scratch regions, sized for the largest chunk so that no region moves between
   // chunks (inside a region the kernels interleave with the chunk's own nsc):
-  //   layer ops | bsub[nb] | xsurf[nb] | planck[nb] | tauc[nb]
-  // Register path: chunk k uses buffer k&1; its back-substitution (side stream)
-  // overlaps chunk k+1, whose tauc/planck prologue (side stream) overlaps chunk k.
-  double* layer_ops = ctx->scratch;
+  //   layer ops[nb] | bsub[nb] | xsurf[nb] | planck[nb] | tauc[nb]
+  // Register path (three streams): chunk k uses buffer k&1; its layer kernel
+  // (stream lay) runs beside chunk k-1's sweep (the caller's stream), its
+  // back-substitution (side stream) beside chunk k+1's layer kernel, and chunk
+  // k+1's tauc/planck prologue (side stream) beside chunk k.
+  double* layer_b[2];
   double* bsub_b[2];
   double* xsurf_b[2];
   double* planck_b[2];
   double* tauc_b[2];
   {
-    double* q = layer_ops + ne1 * nlyr * (size_t)chunk;
+    double* q = ctx->scratch;
+    for (int b = 0; b < nb; ++b, q += ne1 * nlyr * (size_t)chunk) layer_b[b] = q;
     for (int b = 0; b < nb; ++b, q += ne2 * nlyr * (size_t)chunk) bsub_b[b] = q;
     for (int b = 0; b < nb; ++b, q += chunk) xsurf_b[b] = q;
     for (int b = 0; b < nb; ++b) {
@@ -425,6 +436,7 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
     // call (the inputs) -- and, under stream capture, joins the graph here
     HD_HIP(ctx, hipEventRecord(ctx->ev_fork, stream));
     HD_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+    HD_HIP(ctx, hipStreamWaitEvent(ctx->lay, ctx->ev_fork, 0));
   }
   long k = 0;  // chunk index
   for (long s0 = 0; s0 < nsolve; s0 += chunk, ++k) {
@@ -433,19 +445,19 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
     hd::TaucArgs ta;
     hd::PlanckArgs pa;
     prologue_args(s0, nsc, buf, ta, pa);
-    if (!reg || k == 0) {
+    if (!reg) {
       hd::launch_prologue(planck ? &pa : nullptr, beam ? &ta : nullptr, stream);
-    } else {
-      HD_HIP(ctx, hipStreamWaitEvent(stream, ctx->ev_pro[buf], 0));
+    } else if (k == 0) {
+      hd::launch_prologue(planck ? &pa : nullptr, beam ? &ta : nullptr, ctx->side);
+      HD_HIP(ctx, hipEventRecord(ctx->ev_pro[0], ctx->side));
     }
-    if (reg && k >= 2) HD_HIP(ctx, hipStreamWaitEvent(stream, ctx->ev_back[buf], 0));
     hd::LayerArgs la{};
     la.prop = in->prop;
     la.tauc = tauc_b[buf];
     la.fbeam = in->fbeam;
     la.umu0 = in->umu0;
     la.planckv = planck_b[buf];
-    la.scr = layer_ops;
+    la.scr = layer_b[buf];
     la.status = status;
     la.anyerr = ctx->anyerr;
     la.s0 = s0;
@@ -458,7 +470,7 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
     la.max_sweeps = 16;
     la.sink = ctx->sink;
     hd::SweepArgs sa{};
-    sa.scr = layer_ops;
+    sa.scr = layer_b[buf];
     sa.bsub = bsub_b[buf];
     sa.xsurf = xsurf_b[buf];
     sa.flux = flux;
@@ -477,20 +489,40 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
     sa.sink = ctx->sink;
     hipEvent_t* ev = nullptr;
     if (ctx->timing) {
-      if (ctx->pool_used >= 3 * 512) {
+      if (ctx->pool_used >= 4 * 512) {
         rc = resolve_timing(ctx);
         if (rc) return rc;
       }
-      while (ctx->pool.size() < ctx->pool_used + 3) {
+      while (ctx->pool.size() < ctx->pool_used + 4) {
         hipEvent_t e;
         HD_HIP(ctx, hipEventCreate(&e));
         ctx->pool.push_back(e);
       }
       ev = &ctx->pool[ctx->pool_used];
-      ctx->pool_used += 3;
+      ctx->pool_used += 4;
     }
-    hipError_t e = reg ? hd::launch_solve_chunk_nn(nn, nullptr, nullptr, la, sa, stream, ev)
-                       : hd::launch_solve_chunk_team(nn, nullptr, nullptr, la, sa, stream, ev);
+    hipError_t e = hipSuccess;
+    if (reg) {
+      // layer kernel k on `lay`: its inputs (prologue k) are in, and sweep k-2,
+      // the last reader of layer records[buf], is done
+      HD_HIP(ctx, hipStreamWaitEvent(ctx->lay, ctx->ev_pro[buf], 0));
+      if (k >= 2) HD_HIP(ctx, hipStreamWaitEvent(ctx->lay, ctx->ev_sweep[buf], 0));
+      if (ev) HD_HIP(ctx, hipEventRecord(ev[0], ctx->lay));
+      e = hd::launch_layer_nn(nn, la, ctx->lay);
+      if (ev) HD_HIP(ctx, hipEventRecord(ev[1], ctx->lay));
+      HD_HIP(ctx, hipEventRecord(ctx->ev_layer[buf], ctx->lay));
+      // sweep k on the caller's stream: after layer k, and after back-substitution
+      // k-2, the last reader of the back-substitution records[buf]
+      if (e == hipSuccess) {
+        HD_HIP(ctx, hipStreamWaitEvent(stream, ctx->ev_layer[buf], 0));
+        if (k >= 2) HD_HIP(ctx, hipStreamWaitEvent(stream, ctx->ev_back[buf], 0));
+        if (ev) HD_HIP(ctx, hipEventRecord(ev[2], stream));
+        e = hd::launch_sweep_nn(nn, sa, stream);
+        if (ev) HD_HIP(ctx, hipEventRecord(ev[3], stream));
+      }
+    } else {
+      e = hd::launch_solve_chunk_team(nn, nullptr, nullptr, la, sa, stream, ev);
+    }
     if (e != hipSuccess) return fail(ctx, HD_EHIP, "hd_solve: launch failed: %s", hipGetErrorString(e));
     if (reg) {
       HD_HIP(ctx, hipEventRecord(ctx->ev_sweep[buf], stream));

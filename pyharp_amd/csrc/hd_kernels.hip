@@ -48,7 +48,9 @@ __device__ __forceinline__ const Quad<NN>& quad() {
   else return c_quad.q8;
 }
 
-constexpr int kLayerBlock = 256;
+// one wave per block: a layer-kernel wave can take any SIMD the previous chunk's
+// sweep leaves free (hd_solve runs the two on separate streams)
+constexpr int kLayerBlock = 64;
 constexpr int kLayersPerBlock = kLayerBlock / 64;
 
 // phase boundary: keeps the scheduler from hoisting the next phase's loads
@@ -939,6 +941,46 @@ hipError_t launch_solve_chunk_nn(int nn, const PlanckArgs* pa, const TaucArgs* t
   }
 }
 
+template <int NN>
+static void launch_layer(const LayerArgs& la, hipStream_t stream) {
+  const unsigned nb1 = (unsigned)(((la.nsc + 63) / 64) *
+                                  ((la.nlyr + kLayersPerBlock - 1) / kLayersPerBlock));
+  hipLaunchKernelGGL(hd_layer_kernel<NN>, dim3(nb1), dim3(kLayerBlock), 0, stream, la);
+}
+template <int NN>
+static void launch_sweep(const SweepArgs& sa, hipStream_t stream) {
+  hipLaunchKernelGGL(hd_sweep_kernel<NN>, dim3((unsigned)((sa.nsc + 63) / 64)), dim3(64), 0,
+                     stream, sa);
+}
+hipError_t launch_layer_nn(int nn, const LayerArgs& la, hipStream_t stream) {
+  switch (nn) {
+    case 1: launch_layer<1>(la, stream); break;
+    case 2: launch_layer<2>(la, stream); break;
+    case 3: launch_layer<3>(la, stream); break;
+    case 4: launch_layer<4>(la, stream); break;
+    case 5: launch_layer<5>(la, stream); break;
+    case 6: launch_layer<6>(la, stream); break;
+    case 7: launch_layer<7>(la, stream); break;
+    case 8: launch_layer<8>(la, stream); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+hipError_t launch_sweep_nn(int nn, const SweepArgs& sa, hipStream_t stream) {
+  switch (nn) {
+    case 1: launch_sweep<1>(sa, stream); break;
+    case 2: launch_sweep<2>(sa, stream); break;
+    case 3: launch_sweep<3>(sa, stream); break;
+    case 4: launch_sweep<4>(sa, stream); break;
+    case 5: launch_sweep<5>(sa, stream); break;
+    case 6: launch_sweep<6>(sa, stream); break;
+    case 7: launch_sweep<7>(sa, stream); break;
+    case 8: launch_sweep<8>(sa, stream); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 size_t layer_record_doubles(int nn) {
   if (nn <= kMaxRegNN) return (size_t)(nn * (nn + 1) + 2 * nn + 1);
   return (size_t)(2 * nn * nn + 2 * nn + 2);  // team layout: full R, T rows (+ pad to even)
@@ -953,10 +995,10 @@ size_t scratch_doubles_per_solve(int nn, int nlyr, bool planck) {
   // register path: back-substitution records, xsurf and the tauc/planck
   // prologue are double-buffered (chunk k's back-substitution and chunk k+1's
   // prologue run on a side stream beside the main chain), see hd_solve
+  // and the layer records too (chunk k+1's layer kernel runs beside chunk k's sweep)
   const size_t nb = nn <= kMaxRegNN ? 2 : 1;
-  return layer_record_doubles(nn) * nlyr +
-         nb * (bsub_record_doubles(nn) * nlyr + 1 + (planck ? (size_t)nlyr + 3 : 0) +
-               (size_t)nlyr);
+  return nb * (layer_record_doubles(nn) * nlyr + bsub_record_doubles(nn) * nlyr + 1 +
+               (planck ? (size_t)nlyr + 3 : 0) + (size_t)nlyr);
 }
 
 }  // namespace hd

@@ -106,6 +106,9 @@ hipError_t launch_solve_chunk_nn(int nn, const PlanckArgs* pa, const TaucArgs* t
                                  hipEvent_t* ev);
 // back-substitution of a register-path chunk (reads sa.bsub / sa.xsurf)
 hipError_t launch_backsub_nn(int nn, const SweepArgs& sa, hipStream_t stream, bool tail);
+// register path, separately: the layer kernel and the adding sweep of one chunk
+hipError_t launch_layer_nn(int nn, const LayerArgs& la, hipStream_t stream);
+hipError_t launch_sweep_nn(int nn, const SweepArgs& sa, hipStream_t stream);
 hipError_t launch_solve_chunk_team(int nn, const PlanckArgs* pa, const TaucArgs* ta,
                                    const LayerArgs& la, const SweepArgs& sa, hipStream_t stream,
                                    hipEvent_t* ev);

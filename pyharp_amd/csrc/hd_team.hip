@@ -839,11 +839,13 @@ static hipError_t launch_team(const PlanckArgs* pa, const TaucArgs* ta, const La
   const long nt1 = (long)la.nsc * la.nlyr;
   const unsigned nb1 = (unsigned)((nt1 + kTeamsPerBlock - 1) / kTeamsPerBlock);
   const unsigned nb2 = (unsigned)((sa.nsc + kTeamsPerBlock - 1) / kTeamsPerBlock);
+  // timing quadruple: layer start / end, sweep start / end
   if (ev) (void)hipEventRecord(ev[0], stream);
   hipLaunchKernelGGL(hd_team_layer_kernel<NN>, dim3(nb1), dim3(kTeamBlock), 0, stream, la);
   if (ev) (void)hipEventRecord(ev[1], stream);
-  hipLaunchKernelGGL(hd_team_sweep_kernel<NN>, dim3(nb2), dim3(kTeamBlock), 0, stream, sa);
   if (ev) (void)hipEventRecord(ev[2], stream);
+  hipLaunchKernelGGL(hd_team_sweep_kernel<NN>, dim3(nb2), dim3(kTeamBlock), 0, stream, sa);
+  if (ev) (void)hipEventRecord(ev[3], stream);
   return hipGetLastError();
 }
 
