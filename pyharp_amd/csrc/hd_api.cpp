@@ -382,6 +382,10 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
   const int nm = std::max(0, std::min(cfg->nmom, cfg->nprop - 2));
 
   const bool reg = nn <= hd::kMaxRegNN;
+  // a register-path call of one chunk has nothing to overlap: it runs wholly on
+  // the caller's stream (prologue, layer kernel, sweep, tail back-substitution),
+  // without the fork/join of the three-stream pipeline below (C1/C3 latency)
+  const bool single = reg && nsolve <= chunk;
   const bool beam = in->fbeam != nullptr;
   const int nb = reg ? 2 : 1;  // buffers of the per-chunk regions that live across chunks
   // Scratch regions, sized for the largest chunk so that no region moves between
@@ -431,7 +435,7 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
     pa.nlyr = nlyr;
   };
 
-  if (reg) {
+  if (reg && !single) {
     // fork: the side stream sees everything the caller's stream did before this
     // call (the inputs) -- and, under stream capture, joins the graph here
     HD_HIP(ctx, hipEventRecord(ctx->ev_fork, stream));
@@ -445,7 +449,7 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
     hd::TaucArgs ta;
     hd::PlanckArgs pa;
     prologue_args(s0, nsc, buf, ta, pa);
-    if (!reg) {
+    if (!reg || single) {
       hd::launch_prologue(planck ? &pa : nullptr, beam ? &ta : nullptr, stream);
     } else if (k == 0) {
       hd::launch_prologue(planck ? &pa : nullptr, beam ? &ta : nullptr, ctx->side);
@@ -502,7 +506,15 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
       ctx->pool_used += 4;
     }
     hipError_t e = hipSuccess;
-    if (reg) {
+    if (single) {
+      if (ev) HD_HIP(ctx, hipEventRecord(ev[0], stream));
+      e = hd::launch_layer_nn(nn, la, stream);
+      if (ev) HD_HIP(ctx, hipEventRecord(ev[1], stream));
+      if (ev) HD_HIP(ctx, hipEventRecord(ev[2], stream));
+      if (e == hipSuccess) e = hd::launch_sweep_nn(nn, sa, stream);
+      if (ev) HD_HIP(ctx, hipEventRecord(ev[3], stream));
+      if (e == hipSuccess) e = hd::launch_backsub_nn(nn, sa, stream, true);
+    } else if (reg) {
       // layer kernel k on `lay`: its inputs (prologue k) are in, and sweep k-2,
       // the last reader of layer records[buf], is done
       HD_HIP(ctx, hipStreamWaitEvent(ctx->lay, ctx->ev_pro[buf], 0));
@@ -524,7 +536,7 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
       e = hd::launch_solve_chunk_team(nn, nullptr, nullptr, la, sa, stream, ev);
     }
     if (e != hipSuccess) return fail(ctx, HD_EHIP, "hd_solve: launch failed: %s", hipGetErrorString(e));
-    if (reg) {
+    if (reg && !single) {
       HD_HIP(ctx, hipEventRecord(ctx->ev_sweep[buf], stream));
       // next chunk's prologue into the other buffer (free: the side stream already
       // waited for the sweep of chunk k-1, the last user of that buffer)
@@ -544,7 +556,7 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
       HD_HIP(ctx, hipEventRecord(ctx->ev_back[buf], ctx->side));
     }
   }
-  if (reg) {  // the caller's stream sees every chunk's fluxes complete
+  if (reg && !single) {  // the caller's stream sees every chunk's fluxes complete
     for (long b = 0; b < std::min<long>(k, 2); ++b)
       HD_HIP(ctx, hipStreamWaitEvent(stream, ctx->ev_back[b], 0));
   }
