@@ -128,6 +128,32 @@ def test_radiances_vs_oracle(nstr, planck):
     assert rel_err(flux, fref).max() < TOL
 
 
+@pytest.mark.parametrize("numu", [8, 9, 16])
+@pytest.mark.parametrize("nstr,planck", [(4, False), (16, False), (16, True)])
+def test_radiances_many_angles_vs_oracle(numu, nstr, planck):
+    """bench-like angle counts (numu 8 = the bench's, 9 = down/up unbalanced, 16);
+    ncol*nwave*numu not a multiple of the 64-lane block, so the last block is partial"""
+    rng = np.random.default_rng(900 + numu + nstr + 7 * planck)
+    nwave, ncol, nlyr = 2, 5, 7
+    prop, bc, kw = _random_case(rng, nwave, ncol, nlyr, nstr, planck)
+    total = prop[..., 0].sum(axis=-1).min()
+    utau = np.sort(np.concatenate([[0.0, total], rng.uniform(0, total, 2)]))
+    umu = list(np.concatenate([-np.linspace(1.0, 0.12, numu // 2),
+                               np.linspace(0.1, 1.0, numu - numu // 2)]))
+    phi = [0.0, 120.0]
+    d = _disort(nstr, nlyr, nwave, ncol, flags="usrtau,usrang,lamber,quiet", umu=umu, phi=phi,
+                utau=utau, planck=planck, wl=kw.get("wave_lower"), wu=kw.get("wave_upper"))
+    t = None if "temf" not in kw else torch.as_tensor(kw["temf"], device=DEV)
+    flux = d.forward(torch.as_tensor(prop, device=DEV), _dev(bc), t).cpu().numpy()
+    uu = d.get_rad().cpu().numpy()
+    fref, uref = disort_rad_forward(prop, bc, kw.get("temf"), nstr=nstr, umu=umu, phi=phi,
+                                    utau=utau, planck=planck, wave_lower=kw.get("wave_lower"),
+                                    wave_upper=kw.get("wave_upper"))
+    assert uu.shape == uref.shape
+    assert _col_err(uu, uref) < TOL, _col_err(uu, uref)
+    assert rel_err(flux, fref).max() < TOL
+
+
 def test_rayleigh_nonuniform_azimuth_vs_oracle():
     """Rayleigh layers (no delta-M truncation) with a beam: strong azimuth dependence"""
     rng = np.random.default_rng(77)
