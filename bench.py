@@ -203,6 +203,8 @@ def main():
     ap.add_argument("--nstr", type=int, default=None)
     ap.add_argument("--planck", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--chunk", type=int, default=0,
+                    help="max solves per internal chunk (hd_context_set_chunk; 0 = auto)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the solve + band sum as one captured HIP graph per step")
     args = ap.parse_args()
@@ -264,6 +266,8 @@ def main():
         disort.forward(prop, bc, temf, status=status, out=flux)
         band_flux(flux, wts, out=band)
 
+    if args.chunk:
+        _context(dev_index).set_chunk(args.chunk)
     graph = None
     if args.graph:
         solve()  # sizes the context's scratch and tables before capture
@@ -378,7 +382,7 @@ def main():
             "config": {"workload": workload, "ncol": ncol, "ngpoint": G, "nstr": nstr,
                        "nmom": nstr, "nlyr": nlyr, "planck": bool(args.planck),
                        "parallelism": f"spectral g mod {world}",
-                       "hip_graph": bool(args.graph),
+                       "hip_graph": bool(args.graph), "chunk": args.chunk or "auto",
                        "collective": ("all_reduce of the g-weighted band flux (" +
                                       ("gloo, rehearsal" if rehearse else "RCCL") + ")") if world > 1
                        else "none"},
