@@ -115,6 +115,27 @@ struct DisortOptions {
   DisortState ds_;
 };
 
+// Converts pyharp's solver options (`options.disort()`, a pydisort
+// disort::DisortOptions -- or any type with its accessors) into this module's
+// options: the fields pyharp sets at src/radiation/radiation_band.cpp:58-66 plus
+// the header, flags, user depths and ds().nstr/nmom.  This is the one line that
+// changes at radiation_band.cpp:68:
+//   rtsolver = torch::nn::AnyModule(harp_amd::Disort(harp_amd::to_harp_amd(options.disort())));
+template <class PydisortOptions>
+DisortOptions to_harp_amd(PydisortOptions&& src) {
+  DisortOptions op;
+  op.header(src.header()).flags(src.flags()).nwave(src.nwave()).ncol(src.ncol());
+  op.wave_lower(std::vector<double>(src.wave_lower().begin(), src.wave_lower().end()));
+  op.wave_upper(std::vector<double>(src.wave_upper().begin(), src.wave_upper().end()));
+  op.user_tau(std::vector<double>(src.user_tau().begin(), src.user_tau().end()));
+  op.user_mu(std::vector<double>(src.user_mu().begin(), src.user_mu().end()));
+  op.user_phi(std::vector<double>(src.user_phi().begin(), src.user_phi().end()));
+  op.ds().nlyr = src.ds().nlyr;
+  op.ds().nstr = src.ds().nstr;
+  op.ds().nmom = src.ds().nmom;
+  return op;
+}
+
 inline std::set<std::string> parse_flags(const std::string& s) {
   std::set<std::string> out;
   std::stringstream ss(s);
@@ -199,15 +220,22 @@ class DisortImpl : public torch::nn::Cloneable<DisortImpl> {
                    op.has_dtype() ? op.dtype() : rad_.dtype());
   }
 
-  //! flux (nwave, ncol, nlyr+1, 2); level 0 = surface; [..,0] up, [..,1] down
+  //! flux (nwave, ncol, nlyr+1, 2); level 0 = surface; [..,0] up, [..,1] down.
+  //! temf is a Tensor (undefined = none) with a registered default, so
+  //! torch::nn::AnyModule takes both forward(prop, &bc) and
+  //! forward(prop, &bc, layer2level(...)) as radiation_band.cpp:124-127 calls them.
   torch::Tensor forward(torch::Tensor prop, std::map<std::string, torch::Tensor>* bc,
-                        torch::optional<torch::Tensor> temf = torch::nullopt) {
+                        torch::Tensor temf = torch::Tensor()) {
     TORCH_CHECK(prop.dim() == 4, "Disort.forward: prop must be (nwave, ncol, nlyr, nprop)");
     const int nwave = prop.size(0), ncol = prop.size(1), nlyr = prop.size(2),
               nprop = prop.size(3);
     TORCH_CHECK(nlyr == options.ds().nlyr, "Disort.forward: prop has ", nlyr,
                 " layers, ds().nlyr = ", options.ds().nlyr);
-    TORCH_CHECK(!planck_ || temf.has_value(), "Disort.forward: planck flag set but temf missing");
+    TORCH_CHECK(!planck_ || temf.defined(), "Disort.forward: planck flag set but temf missing");
+    TORCH_CHECK(!planck_ || ((int)options.wave_lower().size() == nwave &&
+                             (int)options.wave_upper().size() == nwave),
+                "Disort.forward: planck: prop has ", nwave, " waves but wave_lower/wave_upper hold ",
+                options.wave_lower().size(), "/", options.wave_upper().size());
     auto in_dev = prop.device();
     torch::Device dev = in_dev.is_cuda() ? in_dev : torch::Device(torch::kCUDA, options.device());
     auto f64 = torch::TensorOptions().dtype(torch::kFloat64).device(dev);
@@ -227,7 +255,7 @@ class DisortImpl : public torch::nn::Cloneable<DisortImpl> {
     }
     torch::Tensor tf, wl, wu;
     if (planck_) {
-      tf = to_dev(*temf);
+      tf = to_dev(temf);
       TORCH_CHECK(tf.size(0) == ncol && tf.size(1) == nlyr + 1,
                   "Disort.forward: temf must be (ncol, nlyr+1)");
       wl = torch::tensor(options.wave_lower(), f64);
@@ -269,14 +297,20 @@ class DisortImpl : public torch::nn::Cloneable<DisortImpl> {
     return in_dev.is_cuda() ? flux : flux.to(in_dev);
   }
 
+ protected:
+  FORWARD_HAS_DEFAULT_ARGS({2, torch::nn::AnyValue(torch::Tensor())})
+
  private:
   bool planck_ = false;
   bool onlyfl_ = true, usrtau_ = false, radiance_ = false, corint_ = false;
   std::vector<double> umu_, phi_;
   torch::Tensor rad_;
 
+  // one hd_context per (device, host thread) (SURVEY 8(b) "Threading"); the
+  // modules of a thread share it and libhdisort orders their solves, on any
+  // streams, behind each other
   static hd_context* context(int device) {
-    static std::map<int, std::unique_ptr<hd_context, int (*)(hd_context*)>> ctxs;
+    thread_local std::map<int, std::unique_ptr<hd_context, int (*)(hd_context*)>> ctxs;
     auto it = ctxs.find(device);
     if (it != ctxs.end()) return it->second.get();
     hd_context* c = nullptr;

@@ -51,6 +51,14 @@ struct hd_context {
   bool rad_tables = false;                     // intensity-path constants uploaded
   double* rad_grid = nullptr;                  // device copies of umu | phi | utau
   size_t rad_grid_len = 0;
+  // Serialisation of the context's scratch (SURVEY 8(b) "Threading"): every
+  // entry point holds `mu` while it enqueues, and every solve starts behind
+  // `ev_done`, recorded on the caller's stream at the end of the previous
+  // solve -- so two modules sharing this context from two streams (or two
+  // host threads) never touch scratch/status/anyerr concurrently.
+  std::mutex mu;
+  hipEvent_t ev_done = nullptr;
+  bool done_valid = false;
 };
 
 namespace {
@@ -160,8 +168,14 @@ long auto_chunk(long nsolve, int nn, int nlyr, bool planck) {
   return (nsolve + n - 1) / n;
 }
 
+// the last solve that used the context's buffers has finished (before a free)
+void drain(hd_context* ctx) {
+  if (ctx->done_valid) (void)hipEventSynchronize(ctx->ev_done);
+}
+
 int ensure_scratch(hd_context* ctx, size_t ndoubles) {
   if (ctx->scratch_doubles >= ndoubles) return HD_OK;
+  drain(ctx);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   ctx->scratch = nullptr;
   ctx->scratch_doubles = 0;
@@ -176,6 +190,7 @@ int ensure_scratch(hd_context* ctx, size_t ndoubles) {
 
 int ensure_status(hd_context* ctx, size_t n) {
   if (ctx->status_len >= n) return HD_OK;
+  drain(ctx);
   if (ctx->status) (void)hipFree(ctx->status);
   ctx->status = nullptr;
   ctx->status_len = 0;
@@ -200,6 +215,37 @@ int resolve_timing(hd_context* ctx) {
     ctx->times.sweep_launches += 1;
   }
   ctx->pool_used = 0;
+  return HD_OK;
+}
+
+// restores the caller's current device on every return path (the entry points
+// switch to the context's device)
+struct DeviceGuard {
+  int prev = -1;
+  DeviceGuard() {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// A solve on `stream` starts after the previous solve on this context, whatever
+// stream that one ran on.  Under stream capture the event is neither waited on
+// nor recorded (an event recorded outside the graph cannot order a replay; a
+// captured call is ordered by the stream its graph is replayed on).
+int enter(hd_context* ctx, hipStream_t stream, bool* capturing) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  HD_HIP(ctx, hipStreamIsCapturing(stream, &cs));
+  *capturing = cs != hipStreamCaptureStatusNone;
+  if (!*capturing && ctx->done_valid) HD_HIP(ctx, hipStreamWaitEvent(stream, ctx->ev_done, 0));
+  return HD_OK;
+}
+
+int leave(hd_context* ctx, hipStream_t stream, bool capturing) {
+  if (capturing) return HD_OK;
+  HD_HIP(ctx, hipEventRecord(ctx->ev_done, stream));
+  ctx->done_valid = true;
   return HD_OK;
 }
 
@@ -254,6 +300,7 @@ const char* hd_last_error(const hd_context* ctx) {
 int hd_context_create(hd_context** out, int device) {
   if (!out) return fail(nullptr, HD_EINVAL, "hd_context_create: null out");
   *out = nullptr;
+  DeviceGuard guard;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
     (void)hipGetLastError();
@@ -269,6 +316,7 @@ int hd_context_create(hd_context** out, int device) {
   HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
   HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->lay, hipStreamNonBlocking));
   HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+  HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming));
   HD_HIP(ctx, hipMalloc(&ctx->sink, 4096 * sizeof(double)));
   for (int b = 0; b < 2; ++b) {
     HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_layer[b], hipEventDisableTiming));
@@ -282,7 +330,9 @@ int hd_context_create(hd_context** out, int device) {
 
 int hd_context_destroy(hd_context* ctx) {
   if (!ctx) return HD_OK;
+  DeviceGuard guard;
   (void)hipSetDevice(ctx->device);
+  drain(ctx);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->status) (void)hipFree(ctx->status);
   if (ctx->anyerr) (void)hipFree(ctx->anyerr);
@@ -293,6 +343,7 @@ int hd_context_destroy(hd_context* ctx) {
     if (ctx->ev_pro[b]) (void)hipEventDestroy(ctx->ev_pro[b]);
   }
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+  if (ctx->ev_done) (void)hipEventDestroy(ctx->ev_done);
   if (ctx->sink) (void)hipFree(ctx->sink);
   if (ctx->rad_grid) (void)hipFree(ctx->rad_grid);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
@@ -305,12 +356,14 @@ int hd_context_destroy(hd_context* ctx) {
 
 int hd_context_set_chunk(hd_context* ctx, long max_solves) {
   if (!ctx || max_solves < 0) return fail(ctx, HD_EINVAL, "hd_context_set_chunk: bad args");
+  std::lock_guard<std::mutex> lk(ctx->mu);
   ctx->chunk = max_solves;
   return HD_OK;
 }
 
 int hd_context_set_timing(hd_context* ctx, int enable) {
   if (!ctx) return fail(nullptr, HD_EINVAL, "hd_context_set_timing: null ctx");
+  std::lock_guard<std::mutex> lk(ctx->mu);
   ctx->timing = enable != 0;
   ctx->pool_used = 0;  // (re)start accumulating
   ctx->times = hd_timing{};
@@ -320,6 +373,7 @@ int hd_context_set_timing(hd_context* ctx, int enable) {
 int hd_context_get_timing(const hd_context* ctx_, hd_timing* out) {
   if (!ctx_ || !out) return fail(nullptr, HD_EINVAL, "hd_context_get_timing: null arg");
   hd_context* ctx = const_cast<hd_context*>(ctx_);
+  std::lock_guard<std::mutex> lk(ctx->mu);
   int rc = resolve_timing(ctx);
   if (rc) return rc;
   *out = ctx->times;
@@ -330,6 +384,8 @@ int hd_context_reserve(hd_context* ctx, const hd_config* cfg, long nsolve) {
   if (!ctx || !cfg || nsolve < 0) return fail(ctx, HD_EINVAL, "hd_context_reserve: bad args");
   if (cfg->nstr < 2 || cfg->nstr % 2 || cfg->nstr / 2 > hd::kMaxNN || cfg->nlyr < 1)
     return fail(ctx, HD_EINVAL, "hd_context_reserve: bad config");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard guard;
   HD_HIP(ctx, hipSetDevice(ctx->device));
   const bool planck_r = (cfg->flags & HD_FLAG_PLANCK) != 0;
   const long chunk = ctx->chunk > 0 ? std::min(ctx->chunk, nsolve)
@@ -350,15 +406,16 @@ int hd_quadrature(int nstr, double* mu, double* w) {
   return HD_OK;
 }
 
-int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double* flux,
-             int* status, void* stream_) {
-  if (!ctx) return fail(nullptr, HD_EINVAL, "hd_solve: null context");
-  int rc = validate(ctx, cfg, in, flux);
-  if (rc) return rc;
+}  // extern "C"
+
+namespace {
+
+// hd_solve's enqueue body: everything it launches ends on `stream` (the side
+// and lay streams fork from it and join back into it)
+int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double* flux,
+                  int*& status, hipStream_t stream) {
+  int rc = HD_OK;
   const long nsolve = (long)in->nwave * in->ncol;
-  if (nsolve == 0) return HD_OK;
-  HD_HIP(ctx, hipSetDevice(ctx->device));
-  hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
   const int nn = cfg->nstr / 2;
   const int nlyr = cfg->nlyr;
   const bool planck = (cfg->flags & HD_FLAG_PLANCK) != 0;
@@ -560,22 +617,62 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
     for (long b = 0; b < std::min<long>(k, 2); ++b)
       HD_HIP(ctx, hipStreamWaitEvent(stream, ctx->ev_back[b], 0));
   }
+  return HD_OK;
+}
+
+// The common frame of the two solve entry points: context lock, device guard,
+// ordering behind the context's previous solve, and the synchronous error
+// check when the caller passed no status buffer.
+template <class Enqueue>
+int run_solve(hd_context* ctx, int* status, void* stream_, const char* what, Enqueue&& enqueue) {
+  DeviceGuard guard;
+  HD_HIP(ctx, hipSetDevice(ctx->device));
+  hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+  bool capturing = false;
+  int rc = enter(ctx, stream, &capturing);
+  if (rc) return rc;
+  const bool sync = status == nullptr;
+  rc = enqueue(status, stream);
+  int any = 0;
+  if (rc == HD_OK && sync) {
+    const hipError_t e = hipMemcpyAsync(&any, ctx->anyerr, sizeof(int), hipMemcpyDeviceToHost, stream);
+    if (e != hipSuccess) rc = fail(ctx, HD_EHIP, "%s: anyerr copy: %s", what, hipGetErrorString(e));
+  }
+  const int rc2 = leave(ctx, stream, capturing);  // also after a partial enqueue
+  if (rc) return rc;
+  if (rc2) return rc2;
   if (sync) {
-    int any = 0;
-    HD_HIP(ctx, hipMemcpyAsync(&any, ctx->anyerr, sizeof(int), hipMemcpyDeviceToHost, stream));
     HD_HIP(ctx, hipStreamSynchronize(stream));
     if (any)
       return fail(ctx, HD_ENUMERIC,
-                  "hd_solve: at least one solve failed (bad input, eigen breakdown or non-finite "
-                  "result); DisortWrapper::Run failed.");
+                  "%s: at least one solve failed (bad input, eigen breakdown or non-finite "
+                  "result); DisortWrapper::Run failed.", what);
   }
   return HD_OK;
 }
 
-int hd_solve_radiance(hd_context* ctx, const hd_config* cfg, const hd_inputs* in,
-                      const hd_radiance* rad, double* flux, double* uu, int* status,
-                      void* stream_) {
-  if (!ctx) return fail(nullptr, HD_EINVAL, "hd_solve_radiance: null context");
+}  // namespace
+
+extern "C" {
+
+int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double* flux,
+             int* status, void* stream) {
+  if (!ctx) return fail(nullptr, HD_EINVAL, "hd_solve: null context");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  int rc = validate(ctx, cfg, in, flux);
+  if (rc) return rc;
+  if ((long)in->nwave * in->ncol == 0) return HD_OK;
+  return run_solve(ctx, status, stream, "hd_solve", [&](int*& st, hipStream_t s) {
+    return solve_enqueue(ctx, cfg, in, flux, st, s);
+  });
+}
+
+}  // extern "C"
+
+namespace {
+
+int validate_rad(hd_context* ctx, const hd_config* cfg, const hd_inputs* in,
+                 const hd_radiance* rad, double* flux, double* uu) {
   int rc = validate(ctx, cfg, in, flux);
   if (rc) return rc;
   if (!rad) return fail(ctx, HD_EINVAL, "hd_solve_radiance: null radiance config");
@@ -602,10 +699,20 @@ int hd_solve_radiance(hd_context* ctx, const hd_config* cfg, const hd_inputs* in
         return fail(ctx, HD_EINVAL, "hd_solve_radiance: umu[%d]=%g must be in [-1,0)U(0,1]", i,
                     rad->umu[i]);
   }
+  return HD_OK;
+}
+
+int rad_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in,
+                const hd_radiance* rad, double* flux, double* uu, int*& status,
+                hipStream_t stream) {
+  int rc = HD_OK;
+  const int nn = cfg->nstr / 2;
+  const bool radiances = rad->onlyfl == 0;
+  const int nlyr = cfg->nlyr;
+  const int ntau = rad->ntau > 0 ? rad->ntau : nlyr + 1;
+  const int numu = radiances ? rad->numu : 0;
+  const int nphi = radiances ? rad->nphi : 0;
   const long nsolve = (long)in->nwave * in->ncol;
-  if (nsolve == 0) return HD_OK;
-  HD_HIP(ctx, hipSetDevice(ctx->device));
-  hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
   const bool planck = (cfg->flags & HD_FLAG_PLANCK) != 0;
   const bool beam = in->fbeam != nullptr;
   const bool sync = status == nullptr;
@@ -625,6 +732,7 @@ int hd_solve_radiance(hd_context* ctx, const hd_config* cfg, const hd_inputs* in
   // user grid on the device: umu | phi | utau
   const size_t ngrid = (size_t)numu + nphi + rad->ntau;
   if (ngrid > ctx->rad_grid_len) {
+    drain(ctx);
     if (ctx->rad_grid) (void)hipFree(ctx->rad_grid);
     ctx->rad_grid = nullptr;
     ctx->rad_grid_len = 0;
@@ -735,16 +843,25 @@ int hd_solve_radiance(hd_context* ctx, const hd_config* cfg, const hd_inputs* in
     if (e != hipSuccess)
       return fail(ctx, HD_EHIP, "hd_solve_radiance: launch failed: %s", hipGetErrorString(e));
   }
-  if (sync) {
-    int any = 0;
-    HD_HIP(ctx, hipMemcpyAsync(&any, ctx->anyerr, sizeof(int), hipMemcpyDeviceToHost, stream));
-    HD_HIP(ctx, hipStreamSynchronize(stream));
-    if (any)
-      return fail(ctx, HD_ENUMERIC,
-                  "hd_solve_radiance: at least one solve failed (bad input, eigen breakdown or "
-                  "non-finite result); DisortWrapper::Run failed.");
-  }
   return HD_OK;
 }
+
+}  // namespace
+
+extern "C" {
+
+int hd_solve_radiance(hd_context* ctx, const hd_config* cfg, const hd_inputs* in,
+                      const hd_radiance* rad, double* flux, double* uu, int* status,
+                      void* stream) {
+  if (!ctx) return fail(nullptr, HD_EINVAL, "hd_solve_radiance: null context");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  int rc = validate_rad(ctx, cfg, in, rad, flux, uu);
+  if (rc) return rc;
+  if ((long)in->nwave * in->ncol == 0) return HD_OK;
+  return run_solve(ctx, status, stream, "hd_solve_radiance", [&](int*& st, hipStream_t s) {
+    return rad_enqueue(ctx, cfg, in, rad, flux, uu, st, s);
+  });
+}
+
 
 }  // extern "C"

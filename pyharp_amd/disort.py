@@ -30,6 +30,7 @@ the built library, ``forward`` raises.
 
 from __future__ import annotations
 
+import threading
 from typing import Dict, Optional
 
 import torch
@@ -103,14 +104,21 @@ class DisortOptions:
                 f"ncol={self.ncol()}, ds={self._ds})")
 
 
-_CONTEXTS: Dict[int, _lib.Context] = {}
+_THREAD = threading.local()
 
 
 def _context(device: int) -> _lib.Context:
-    ctx = _CONTEXTS.get(device)
+    """The calling host thread's hd_context on ``device`` (SURVEY 8(b) "Threading":
+    one context per (device, host thread)).  Modules of one thread share it; the
+    library orders their solves on any streams behind each other (hd_solve waits
+    for the context's previous solve), so scratch is never used twice at once."""
+    ctxs = getattr(_THREAD, "contexts", None)
+    if ctxs is None:
+        ctxs = _THREAD.contexts = {}
+    ctx = ctxs.get(device)
     if ctx is None:
         ctx = _lib.Context(device)
-        _CONTEXTS[device] = ctx
+        ctxs[device] = ctx
     return ctx
 
 
@@ -205,6 +213,11 @@ class Disort(RTSolver):
                 raise RuntimeError(f"Disort.forward: unknown boundary condition '{k}'")
         if self.planck and temf is None:
             raise RuntimeError("Disort.forward: planck flag set but temf not given")
+        if self.planck and not (nwave == len(op.wave_lower()) == len(op.wave_upper())):
+            # the kernels read wave_lower/upper[w] for every w < prop.shape[0]
+            raise RuntimeError(f"Disort.forward: planck: prop has {nwave} waves but "
+                               f"wave_lower/wave_upper hold {len(op.wave_lower())}/"
+                               f"{len(op.wave_upper())}")
         if not torch.cuda.is_available():
             raise RuntimeError("Disort.forward: no HIP device available (pyharp_amd has no "
                                "CPU path)")

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Compile the C++ drop-in checks against the container's libtorch (ROCm build)
 # and the in-tree libhdisort.so.  Outputs: tests/cpp/disort_dropin, tests/cpp/amars_sw_dropin,
-# tests/cpp/disort_rad_dropin, tests/cpp/amars_lw_dropin
+# tests/cpp/disort_rad_dropin, tests/cpp/amars_lw_dropin, tests/cpp/radiation_band_swap
 set -euo pipefail
 HERE=$(cd "$(dirname "$0")" && pwd)
 ROOT=$(cd "$HERE/../.." && pwd)
@@ -18,4 +18,5 @@ build disort_dropin &
 build amars_sw_dropin &
 build disort_rad_dropin &
 build amars_lw_dropin &
-wait %1 && wait %2 && wait %3 && wait %4
+build radiation_band_swap &
+wait %1 && wait %2 && wait %3 && wait %4 && wait %5

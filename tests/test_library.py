@@ -134,6 +134,21 @@ def test_forward_shape_errors():
         d.forward(torch.zeros((1, 1, 3, 6), dtype=torch.float64), {"fbam": torch.ones(1, 1)})
 
 
+def test_planck_wave_count_must_match_prop():
+    """With planck the kernels read wave_lower/upper[w] for every w < prop.shape[0]:
+    a prop with more (or fewer) waves than the options' bounds is refused."""
+    from pyharp_amd import Disort, DisortOptions
+    op = DisortOptions().flags("lamber,onlyfl,planck").nwave(2).ncol(1)
+    op.wave_lower([1.0, 2.0]).wave_upper([2.0, 3.0])
+    op.ds().nlyr, op.ds().nstr = 3, 4
+    d = Disort(op)
+    temf = torch.full((1, 4), 250.0, dtype=torch.float64)
+    with pytest.raises(RuntimeError, match="waves"):
+        d.forward(torch.zeros((3, 1, 3, 6), dtype=torch.float64), {}, temf)
+    with pytest.raises(RuntimeError, match="waves"):
+        d.forward(torch.zeros((1, 1, 3, 6), dtype=torch.float64), {}, temf)
+
+
 def test_layer2level_torch_matches_reference_run():
     from pyharp_amd import layer2level
     out = layer2level(torch.tensor([[300.0, 280.0, 260.0, 250.0, 240.0]], dtype=torch.float64))
