@@ -25,7 +25,8 @@
  *          amars_lw.cpp:73-74)
  *   temf  [ncol][nlyr+1] f64 level temperatures, level 0 = bottom (planck)
  *         (amars_lw.cpp:76, src/utils/layer2level.hpp:41)
- *   wave_lower/upper [nwave] f64 wavenumber bounds [cm^-1] (planck)
+ *   wave_lower/upper [nwave] f64 wavenumber bounds [cm^-1] (planck): one entry
+ *         per wave of prop -- the kernels read index w for every w < nwave
  *   flux  [nwave][ncol][nlyr+1][2] f64, level 0 = surface,
  *         [..][0] = upward flux, [..][1] = rfldir + rfldn
  *         (src/rtsolver/rt_solver_disort.cpp_:172-181, amars_sw.cpp:185-191)
@@ -33,6 +34,15 @@
  *
  * Errors never cross the ABI as exceptions: every entry point returns an
  * hd_status code; hd_last_error() gives the message.
+ *
+ * Threading: a context may be shared by several modules, streams
+ * and host threads.  Each entry point holds the context's mutex while it
+ * enqueues, and every solve starts behind the previous solve on the context
+ * (an event on that solve's stream), so the context's scratch is never used by
+ * two solves at once.  Calls captured into a HIP graph are ordered by the
+ * stream the graph is replayed on instead.  The entry points restore the
+ * caller's current device.  For concurrency across host threads use one context
+ * per (device, thread), as the bindings do.
  */
 #ifndef HDISORT_H_
 #define HDISORT_H_
