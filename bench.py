@@ -1,6 +1,6 @@
 """Benchmark of the DISORT flux hot path on MI355X (driver contract).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c5] [--planck]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c5|c1|c3|c3l] [--planck]
                     [--ncol C] [--ngpoint G]
 
 Default workload (BASELINE.json configs[3], SURVEY.md 8(d) "C4 GCM", the
@@ -73,6 +73,9 @@ CONFIGS = {
                label="C1 amars_lw ck (synthetic k)"),
     "c3": dict(ncol=1, ngpoint=19990, nstr=8, nlyr=40, lw=True, tau=(1e-5, 5.0),
                band=(1.0, 2000.0), label="C3 line-by-line (synthetic k)"),
+    # BASELINE.json configs[2] "~1e5 spectral points": 0.1 cm^-1 bins tiling [1, 10001]
+    "c3l": dict(ncol=1, ngpoint=100000, nstr=8, nlyr=40, lw=True, tau=(1e-5, 5.0),
+                band=(1.0, 10001.0), label="C3 line-by-line 1e5 bins (synthetic k)"),
 }
 
 

@@ -335,6 +335,18 @@ def test_c3_line_by_line_shape(oracle_c):
     assert rel_err(f, ref).max() < TOL
 
 
+def test_c3_line_by_line_1e5(oracle_c):
+    """C3 at the BASELINE.json size (configs[2]: "~1e5 spectral points"): 1 column,
+    100 000 bins of 0.1 cm^-1 tiling [1, 10001], nstr=8, nlyr=40, omega=0, Planck --
+    every bin against the C oracle (two internal chunks of 50 000 solves)."""
+    G = 100000
+    prop, bc, temf, wl, wu = _lw_problem(G, 8, 40, (1e-5, 5.0), (1.0, 10001.0), ck=False)
+    d = _disort(8, 40, G, 1, planck=True, wl=wl, wu=wu)
+    f = _run(d, prop, bc, temf)
+    ref = oracle_c.forward(prop, bc, temf, nstr=8, planck=True, wave_lower=wl, wave_upper=wu)
+    assert rel_err(f, ref).max() < TOL
+
+
 @pytest.mark.parametrize("nstr", [8, 32])
 def test_graph_capture_replay(nstr):
     """hd_solve is stream-ordered and allocation-free once the context is
