@@ -383,7 +383,10 @@ def main():
                 f"nlyr={nlyr}, " + ("thermal (planck), omega=0" if lw else
                                     f"beam{' + planck' if args.planck else ''}"))
 
-    layer_kernel = "hd_layer_kernel" if nstr <= 16 else "hd_team_layer_kernel"
+    team_valu = os.environ.get("HD_TEAM_LAYER") == "valu"  # A/B switch of the team path
+    layer_kernel = ("hd_layer_kernel" if nstr <= 16 else
+                    "hd_team_layer_kernel" if team_valu else "hd_team_mfma_layer_kernel")
+    mfma = nstr > 16 and not team_valu
     if rank == 0:
         # dominant kernel roofline (the layer-setup kernel), per launch
         k1_avg_ms = tm.layer_ms / max(tm.layer_launches, 1)
@@ -395,7 +398,7 @@ def main():
             k1 = pmc["kernels"].get(f"{layer_kernel}<{nstr // 2}>")
             if k1:
                 traffic = round(k1["bytes_per_solve"] * solves_per_launch)
-        roofline = {"bound": "fp64-valu", "kernel": f"{layer_kernel}<{nstr // 2}>", "achieved": round(ach, 3),
+        roofline = {"bound": "fp64-mfma+valu" if mfma else "fp64-valu", "kernel": f"{layer_kernel}<{nstr // 2}>", "achieved": round(ach, 3),
                     "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(ach / FP64_PEAK_TFLOPS, 4),
                     "traffic": traffic,
@@ -406,8 +409,11 @@ def main():
                     "(89 doubles per layer) are written to HBM scratch for the sweep",
                     "avg_launch_ms": round(k1_avg_ms, 3),
                     "flop_per_solve": k1_flop,
-                    "note": "FP64 compute bound, VALU (no MFMA in this kernel; gfx950's FP64 "
-                            "vector and MFMA peaks are both 78.6 TF/s); achieved uses the SURVEY 8(d) algorithmic FLOP convention"
+                    "note": ("FP64 compute bound: dense 16x16 products on FP64 MFMA, the "
+                             "Cholesky/Jacobi/triangular algebra on the VALU (gfx950's FP64 "
+                             "vector and MFMA peaks are both 78.6 TF/s)" if mfma else
+                             "FP64 compute bound, VALU (no MFMA in this kernel; gfx950's FP64 "
+                             "vector and MFMA peaks are both 78.6 TF/s)") + "; achieved uses the SURVEY 8(d) algorithmic FLOP convention"
                             + ("; nstr<=16: each launch runs on its own stream beside the "
                                "previous chunk's sweep, so its duration includes that "
                                "co-running (path_roofline is what the throughput follows)"

@@ -25,283 +25,18 @@
 // Scratch records, solve-major inside a layer (a team's record is contiguous):
 //   layer ops [lc][s][2NN^2+2NN+2]  R~ rows | T~ rows | S~+ | S~- | tau' | pad
 //   back-sub  [lc][s][NN^2+2NN+1 -> even]  ZT rows | t | rc | cs | pad
-#include <utility>
+#include <cstdlib>
+#include <cstring>
 
-#include "hd_kernels.hpp"
+#include "hd_team_prims.hpp"
 
 namespace hd {
 
-struct QuadTablesTeam {
-  Quad<9> q9;
-  Quad<10> q10;
-  Quad<11> q11;
-  Quad<12> q12;
-  Quad<13> q13;
-  Quad<14> q14;
-  Quad<15> q15;
-  Quad<16> q16;
-};
-__constant__ QuadTablesTeam c_quad_team;
-
-template <int NN>
-__device__ __forceinline__ const Quad<NN>& tquad() {
-  if constexpr (NN == 9) return c_quad_team.q9;
-  else if constexpr (NN == 10) return c_quad_team.q10;
-  else if constexpr (NN == 11) return c_quad_team.q11;
-  else if constexpr (NN == 12) return c_quad_team.q12;
-  else if constexpr (NN == 13) return c_quad_team.q13;
-  else if constexpr (NN == 14) return c_quad_team.q14;
-  else if constexpr (NN == 15) return c_quad_team.q15;
-  else return c_quad_team.q16;
-}
-
 namespace {
-
-constexpr int kTeam = 16;
-constexpr int kTeamBlock = 256;
-constexpr int kTeamsPerBlock = kTeamBlock / kTeam;
-
-// ---- compile-time loops (DPP controls must be immediates) -------------------
-template <int B, class F, int... Is>
-__device__ __forceinline__ void sfor_impl(F&& f, std::integer_sequence<int, Is...>) {
-  (f(std::integral_constant<int, B + Is>{}), ...);
-}
-// f(k) for k = B .. E-1 (ascending)
-template <int B, int E, class F>
-__device__ __forceinline__ void sfor(F&& f) {
-  if constexpr (E > B) sfor_impl<B>(f, std::make_integer_sequence<int, E - B>{});
-}
-template <int B, class F, int... Is>
-__device__ __forceinline__ void sfor_rev_impl(F&& f, std::integer_sequence<int, Is...>) {
-  (f(std::integral_constant<int, B - Is>{}), ...);
-}
-// f(k) for k = E-1 .. B (descending)
-template <int B, int E, class F>
-__device__ __forceinline__ void sfor_rev(F&& f) {
-  if constexpr (E > B) sfor_rev_impl<E - 1>(f, std::make_integer_sequence<int, E - B>{});
-}
-#define HD_K(x) decltype(x)::value
-
-// ---- DPP primitives ----------------------------------------------------------
-__device__ __forceinline__ int tlane() { return (int)(threadIdx.x & (kTeam - 1)); }
-
-template <int CTRL>
-__device__ __forceinline__ double dpp(double x) {
-  return __builtin_amdgcn_update_dpp(0.0, x, CTRL, 0xF, 0xF, true);  // every source lane valid
-}
-// value held by team lane K (row_newbcast:K)
-template <int K>
-__device__ __forceinline__ double bc(double x) {
-  return dpp<0x150 + K>(x);
-}
-constexpr int quad_xor(int m) {
-  return (0 ^ m) | ((1 ^ m) << 2) | ((2 ^ m) << 4) | ((3 ^ m) << 6);
-}
-// value held by team lane (i ^ M): XOR masks compose, so M = hi ^ lo is built
-// from row_half_mirror (^7), row_ror:8 (^8), row_mirror (^15) and a quad_perm
-template <int M>
-__device__ __forceinline__ double xperm(double x) {
-  static_assert(M > 0 && M < 16, "team XOR mask");
-  constexpr int hi = M & 12;
-  constexpr int lo = (hi == 4 || hi == 12) ? ((M & 3) ^ 3) : (M & 3);
-  if constexpr (hi == 4) x = dpp<0x141>(x);
-  else if constexpr (hi == 8) x = dpp<0x128>(x);
-  else if constexpr (hi == 12) x = dpp<0x140>(x);
-  if constexpr (lo != 0) x = dpp<quad_xor(lo)>(x);
-  return x;
-}
-// value held by team lane (i ^ M) through the LDS crossbar (ds_swizzle, bit
-// mode: and 0x1f, xor M inside each 32-lane half): no LDS storage, and the
-// exchange issues on the LDS pipe instead of the VALU the Jacobi rounds saturate
-template <int M>
-__device__ __forceinline__ double xswz(double x) {
-  static_assert(M > 0 && M < 16, "team XOR mask");
-  constexpr int pat = 0x1F | (M << 10);
-  const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(x), pat);
-  const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(x), pat);
-  return __hiloint2double(hi, lo);
-}
-// sum over the 16 lanes of the team (every lane receives a sum; the
-// association differs per lane, so take bc<0>() where a uniform value matters)
-__device__ __forceinline__ double team_sum(double x) {
-  x += dpp<0x128>(x);
-  x += dpp<0x124>(x);
-  x += dpp<0x122>(x);
-  x += dpp<0x121>(x);
-  return x;
-}
-
-// ---- team linear algebra (lane i = row i) ------------------------------------
-
-// Cholesky of the SPD matrix whose row i lane i holds in a.  Out: a = row i of
-// L (zeros above the diagonal); lt = row i of L^T (column i of L) if WANT_LT;
-// rd = 1/L_ii.  Returns false on a non-positive pivot (uniform over the team).
-template <int NN, bool WANT_LT>
-__device__ __forceinline__ bool team_chol(double (&a)[NN], double (&lt)[NN], double& rd) {
-  const int i = tlane();
-  bool ok = true;
-  rd = 0.0;
-  if constexpr (WANT_LT) sfor<0, NN>([&](auto J) { lt[HD_K(J)] = 0.0; });
-  sfor<0, NN>([&](auto K) {
-    constexpr int k = HD_K(K);
-    double d = bc<k>(a[k]);
-    ok = ok && d > 0.0;
-    d = d > 1.0e-300 ? d : 1.0e-300;
-    const double r = rsq_nr(d);
-    const double lkk = d * r;
-    const double aik = a[k] * r;
-    a[k] = i > k ? aik : (i == k ? lkk : 0.0);
-    if (i == k) rd = r;
-    if constexpr (WANT_LT) {
-      if (i == k) lt[k] = lkk;
-    }
-    sfor<k + 1, NN>([&](auto J) {
-      constexpr int j = HD_K(J);
-      const double ljk = bc<j>(a[k]);
-      a[j] = fma(-a[k], ljk, a[j]);  // above the diagonal: zeroed at step j
-      if constexpr (WANT_LT) {
-        if (i == k) lt[j] = ljk;
-      }
-    });
-  });
-  return ok;
-}
-
-// x <- L^-1 x  (x distributed: lane i holds x_i)
-template <int NN>
-__device__ __forceinline__ void team_lsolve(const double (&l)[NN], double rd, double& x) {
-  const int i = tlane();
-  sfor<0, NN>([&](auto K) {
-    constexpr int k = HD_K(K);
-    if (i == k) x *= rd;
-    const double xk = bc<k>(x);
-    if (i > k) x = fma(-l[k], xk, x);
-  });
-}
-
-// x <- L^-T x  (lt = rows of L^T)
-template <int NN>
-__device__ __forceinline__ void team_usolve(const double (&lt)[NN], double rd, double& x) {
-  const int i = tlane();
-  sfor_rev<0, NN>([&](auto K) {
-    constexpr int k = HD_K(K);
-    if (i == k) x *= rd;
-    const double xk = bc<k>(x);
-    if (i < k) x = fma(-lt[k], xk, x);
-  });
-}
-
-// X <- L^-T X  (X rows distributed)
-template <int NN>
-__device__ __forceinline__ void team_umsolve(const double (&lt)[NN], double rd, double (&x)[NN]) {
-  const int i = tlane();
-  sfor_rev<0, NN>([&](auto K) {
-    constexpr int k = HD_K(K);
-    const double sc = i == k ? rd : 1.0;
-    sfor<0, NN>([&](auto J) { x[HD_K(J)] *= sc; });
-    const double m = i < k ? lt[k] : 0.0;
-    sfor<0, NN>([&](auto J) {
-      constexpr int j = HD_K(J);
-      x[j] = fma(-m, bc<k>(x[j]), x[j]);
-    });
-  });
-}
-
-// ---- Jacobi eigensolver, XOR parallel ordering --------------------------------
-// Round M pairs lane i with lane i^M; rounds 1..15 cover every pair once.
-template <int NN>
-__host__ __device__ constexpr bool round_has_pair(int m) {
-  for (int p = 0; p < NN; ++p)
-    if ((p ^ m) > p && (p ^ m) < NN) return true;
-  return false;
-}
-
-// One-sided (Hestenes) Jacobi on the columns of B: lane j holds column j of B.
-// Round M rotates the column pair (j, j^M) to make the two orthogonal --
-// exactly the two-sided Jacobi rotation of B^T B for that pair, built from
-// column dot products -- so B^T B is never formed and no diagonal has to be
-// fished out of a lane-indexed register.  Both lanes of a pair form their
-// operands in the same order (products commute exactly), so the two rotations
-// agree bitwise.  The rotations are not accumulated: with B = B0 V the
-// eigenvectors come out afterwards as V = B0^-1 B (two triangular solves, see
-// the layer kernel), which removes half of the cross-lane traffic per round.
-constexpr double kJacobiTol2 = 1.0e-30;  // rotate while (b_p.b_q)^2 > tol |b_p|^2 |b_q|^2
-// the last sweep needed: the one whose off-diagonal Frobenius norm of B^T B
-// (accumulated from the pairs' b_p.b_q as they were rotated) stayed below 1e-8
-// of its diagonal -- quadratic convergence leaves ~1e-16 after it (the register
-// path's jacobi_os rule; at nstr = 32 one sweep fewer than a per-pair 1e-9 cosine
-// bound for the same residual, ~4e-15)
-constexpr double kJacobiLastFrob2 = 1.0e-16;
-
-template <int NN, int M>
-__device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double& own, bool on,
-                                                  double& off) {
-  const int i = tlane();
-  const int pi = i ^ M;
-  double bq[NN];
-  sfor<0, NN>([&](auto K) { bq[HD_K(K)] = xswz<M>(b[HD_K(K)]); });
-  const double oth = xswz<M>(own);  // |b_partner|^2, tracked by the partner
-  double g0 = 0.0, g1 = 0.0;  // two chains: the partner columns arrive in order
-  sfor<0, NN>([&](auto K) {
-    constexpr int k = HD_K(K);
-    if constexpr (k % 2 == 0) g0 = fma(b[k], bq[k], g0);
-    else g1 = fma(b[k], bq[k], g1);
-  });
-  const double gam = g0 + g1;
-  const bool lo = i < pi;
-  const double app = lo ? own : oth;
-  const double aqq = lo ? oth : own;
-  const bool pair = i < NN && pi < NN;
-  const double g2 = gam * gam, pq = app * aqq;
-  const bool r = on && pair && g2 > kJacobiTol2 * pq;
-  off += pair ? g2 : 0.0;  // each pair counted by both of its lanes
-  // w = sqrt(d^2 + 4 g^2), u = |d| + w, z = 1/sqrt(2 w u): c = u z, s = sgn(d) 2 g z
-  const double d = aqq - app;
-  const double w2 = r ? fma(d, d, 4.0 * g2) : 1.0;
-  const double w = w2 * rsq_nr1(w2);
-  const double u = fabs(d) + w;
-  const double z = rsq_nr1(2.0 * w * u);
-  const double sg = d < 0.0 ? -2.0 : 2.0;
-  const double c = r ? u * z : 1.0;
-  const double s = r ? sg * gam * z : 0.0;
-  const double se = lo ? -s : s;  // p side: c b_p - s b_q ; q side: s b_p + c b_q
-  sfor<0, NN>([&](auto K) { b[HD_K(K)] = fma(se, bq[HD_K(K)], c * b[HD_K(K)]); });
-  // rotated norms: |c b_p - s b_q|^2 and |s b_p + c b_q|^2
-  const double cc = c * c, ss2 = s * s, cs2 = 2.0 * c * s * gam;
-  own = lo ? fma(cc, app, fma(ss2, aqq, -cs2)) : fma(ss2, app, fma(cc, aqq, cs2));
-}
-
-// Sweeps of rounds 1..15 until the sweep that was the last one needed
-// (kJacobiLastFrob2), or max_sweeps.  A converged team issues no-op rotations
-// (c = 1, s = 0) while its wave-mates finish.
-template <int NN>
-__device__ __forceinline__ void team_jacobi(double (&b)[NN], int max_sweeps) {
-  bool on = true;
-  for (int sweep = 0; sweep < max_sweeps; ++sweep) {
-    double off = 0.0;  // this lane's sum of (b_p.b_q)^2 over its pairs in this sweep
-    double own = 0.0;  // |b_j|^2, exact at the start of every sweep, then tracked
-    sfor<0, NN>([&](auto K) { own = fma(b[HD_K(K)], b[HD_K(K)], own); });
-    const double dia = bc<0>(team_sum(own * own));  // sum_j |b_j|^4 (team-uniform)
-    sfor<1, kTeam>([&](auto Mc) {
-      constexpr int m = HD_K(Mc);
-      if constexpr (round_has_pair<NN>(m)) team_jacobi_round<NN, m>(b, own, on, off);
-    });
-    // every pair was counted twice (once per lane): compare 2x the bound
-    on = on && bc<0>(team_sum(off)) > 2.0 * kJacobiLastFrob2 * dia;
-    if (__all(!on)) break;
-  }
-}
-
+__constant__ QuadTablesTeam c_quad_team;
 }  // namespace
 
-template <int NN>
-constexpr int ne1t() {
-  return 2 * NN * NN + 2 * NN + 2;
-}
-template <int NN>
-constexpr int ne2t() {
-  return (NN * NN + 2 * NN + 2) & ~1;
-}
+using namespace team;
 
 // ============================================================================
 // K1 (team): per-(solve, layer) setup
@@ -310,7 +45,7 @@ template <int NN>
 __global__ __launch_bounds__(kTeamBlock) void hd_team_layer_kernel(LayerArgs A) {
   __shared__ double tr_lds[kTeamsPerBlock * kTeam * (kTeam + 1)];  // 16 transpose tiles
   constexpr int N = 2 * NN;
-  const Quad<NN>& Qc = tquad<NN>();
+  const Quad<NN>& Qc = tquad<NN>(c_quad_team);
   const int i = tlane();
   const bool act = i < NN;
   const int ii = act ? i : 0;
@@ -608,7 +343,7 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_layer_kernel(LayerArgs A) 
 // ============================================================================
 template <int NN>
 __global__ __launch_bounds__(kTeamBlock) void hd_team_sweep_kernel(SweepArgs A) {
-  const Quad<NN>& Qc = tquad<NN>();
+  const Quad<NN>& Qc = tquad<NN>(c_quad_team);
   const int i = tlane();
   const bool act = i < NN;
   const int ii = act ? i : 0;
@@ -818,8 +553,7 @@ static void fill_quad_team(Quad<NN>& q, const QuadHost& h) {
   }
 }
 
-hipError_t upload_quad_tables_team(const QuadHost* per_nn /* [kMaxNN], index nn-1 */) {
-  QuadTablesTeam t;
+void fill_quad_tables_team(const QuadHost* per_nn, QuadTablesTeam& t) {
   fill_quad_team<9>(t.q9, per_nn[8]);
   fill_quad_team<10>(t.q10, per_nn[9]);
   fill_quad_team<11>(t.q11, per_nn[10]);
@@ -828,7 +562,24 @@ hipError_t upload_quad_tables_team(const QuadHost* per_nn /* [kMaxNN], index nn-
   fill_quad_team<14>(t.q14, per_nn[13]);
   fill_quad_team<15>(t.q15, per_nn[14]);
   fill_quad_team<16>(t.q16, per_nn[15]);
-  return hipMemcpyToSymbol(HIP_SYMBOL(c_quad_team), &t, sizeof(t), 0, hipMemcpyHostToDevice);
+}
+
+hipError_t upload_quad_tables_team(const QuadHost* per_nn /* [kMaxNN], index nn-1 */) {
+  QuadTablesTeam t;
+  fill_quad_tables_team(per_nn, t);
+  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_quad_team), &t, sizeof(t), 0, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = upload_quad_tables_team_mfma(t);
+  return e;
+}
+
+// HD_TEAM_LAYER=valu selects the VALU-product layer kernel (A/B runs); the
+// default is the MFMA one (hd_team_mfma.hip)
+static bool team_layer_valu() {
+  static const bool v = [] {
+    const char* e = std::getenv("HD_TEAM_LAYER");
+    return e && std::strcmp(e, "valu") == 0;
+  }();
+  return v;
 }
 
 template <int NN>
@@ -841,7 +592,12 @@ static hipError_t launch_team(const PlanckArgs* pa, const TaucArgs* ta, const La
   const unsigned nb2 = (unsigned)((sa.nsc + kTeamsPerBlock - 1) / kTeamsPerBlock);
   // timing quadruple: layer start / end, sweep start / end
   if (ev) (void)hipEventRecord(ev[0], stream);
-  hipLaunchKernelGGL(hd_team_layer_kernel<NN>, dim3(nb1), dim3(kTeamBlock), 0, stream, la);
+  if (team_layer_valu()) {
+    hipLaunchKernelGGL(hd_team_layer_kernel<NN>, dim3(nb1), dim3(kTeamBlock), 0, stream, la);
+  } else {
+    const hipError_t e = launch_team_layer_mfma(NN, la, stream);
+    if (e != hipSuccess) return e;
+  }
   if (ev) (void)hipEventRecord(ev[1], stream);
   if (ev) (void)hipEventRecord(ev[2], stream);
   hipLaunchKernelGGL(hd_team_sweep_kernel<NN>, dim3(nb2), dim3(kTeamBlock), 0, stream, sa);

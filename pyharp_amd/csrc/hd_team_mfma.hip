@@ -1,0 +1,491 @@
+// hd_team_mfma.hip -- per-(solve, layer) setup for nstr 18..32 with the dense
+// 16 x 16 products on FP64 MFMA (v_mfma_f64_16x16x4_f64).
+//
+//   hd_team_mfma_layer_kernel<NN>  one wave = four (solve, layer) problems, the
+//                                  same per-layer setup as hd_team_layer_kernel
+//                                  (delta-M, phase matrix, Cholesky + one-sided
+//                                  Jacobi eigenproblem, beam/thermal particular
+//                                  solutions, R~/T~/S~ in the flux-weighted
+//                                  basis)  [c_setdis,
+//                                  c_soleig, c_upbeam, c_upisot]
+//
+// The work splits by shape:
+//   * sequential, one-problem-per-team algebra stays on the VALU in the team
+//     layout (T: team t = lanes 16t..16t+15, lane i holds row i): phase-matrix
+//     rows, the four Cholesky factorisations (S-, S+, I + Omega Omega^T,
+//     I + Psi^T Psi), their triangular inverses, the Jacobi sweeps and the
+//     vector recurrences of the particular solutions;
+//   * every dense 16 x 16 product runs on the matrix core in the MFMA layout
+//     (M: for problem t, lane 16h + c holds X_t[h + 4m][c] in register m), four
+//     k-steps per product and problem:
+//        B0^T = L^T C            (Jacobi input)
+//        U    = C^-T B,  U^T = B^T C^-1
+//        W    = L^-T L^-1        (= (-A-)^-1)
+//        Psi  = Gamma^1/2 U^T W,  Omega^T = Delta^1/2 U^T
+//        I + Omega Omega^T,  I + Psi^T Psi
+//        A-   = K-^T K-,  A+ = K+^T K+   (K = J^-1, J J^T = I + ...)
+//     MFMA needs no cross-lane broadcasts: the operand of k-step s of A.B is
+//     register s of A^T and of B in the M layout, and the product comes out in
+//     the M layout, so chains of products need no data movement.  T <-> M goes
+//     through two LDS tile-sets per wave (row stride 17 doubles).
+//
+// Replaces the DPP-broadcast products of hd_team_layer_kernel, whose row
+// broadcasts, 64-bit selects and register spills were 39% of its VALU
+// instructions at one wave per SIMD (profiles/r02_c5_team_counters_v1.json).
+#include "hd_team_prims.hpp"
+
+namespace hd {
+
+namespace {
+
+__constant__ QuadTablesTeam c_qt;
+
+using namespace team;
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int kS = 17;           // tile row stride (doubles): conflict-free row and column reads
+constexpr int kTile = 16 * kS;   // one problem's 16 x 16 tile
+constexpr int kSet = 4 * kTile;  // a wave's four problems
+
+// ---- T <-> LDS <-> M ----------------------------------------------------------
+// T row i of team t -> tile_t[i][0..NN)
+template <int NN>
+__device__ __forceinline__ void put_rows(double* ts, int t, int i, const double (&x)[NN]) {
+  double* r = ts + t * kTile + i * kS;
+  sfor<0, NN>([&](auto J) { r[HD_K(J)] = x[HD_K(J)]; });
+}
+template <int NN>
+__device__ __forceinline__ void get_rows(const double* ts, int t, int i, double (&x)[NN]) {
+  const double* r = ts + t * kTile + i * kS;
+  sfor<0, NN>([&](auto J) { x[HD_K(J)] = r[HD_K(J)]; });
+}
+// column i of tile_t -> x (the row of the transposed matrix)
+template <int NN>
+__device__ __forceinline__ void get_cols(const double* ts, int t, int i, double (&x)[NN]) {
+  const double* r = ts + t * kTile + i;
+  sfor<0, NN>([&](auto J) { x[HD_K(J)] = r[HD_K(J) * kS]; });
+}
+// M layout of every problem: X[t][m] = tile_t[h + 4m][c]
+__device__ __forceinline__ void put_m(double* ts, int h, int c, const double (&x)[4][4]) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) ts[t * kTile + (h + 4 * m) * kS + c] = x[t][m];
+}
+__device__ __forceinline__ void get_m(const double* ts, int h, int c, double (&x)[4][4]) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) x[t][m] = ts[t * kTile + (h + 4 * m) * kS + c];
+}
+// M layout of the transposed tiles: X[t][m] = tile_t[c][h + 4m]
+__device__ __forceinline__ void get_mt(const double* ts, int h, int c, double (&x)[4][4]) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) x[t][m] = ts[t * kTile + c * kS + h + 4 * m];
+}
+// LDS reads of one wave complete in order after its writes; this keeps the
+// compiler from moving LDS accesses -- or anything else: the scheduler would
+// hoist the next phase's loads and their registers -- across phase boundaries
+__device__ __forceinline__ void lds_fence() {
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// D_t = A_t B_t (+ I) for the wave's four problems; at = A^T and b = B in M
+template <bool ADD_I>
+__device__ __forceinline__ void mprod(const double (&at)[4][4], const double (&b)[4][4],
+                                      double (&d)[4][4], int h, int c) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    d4 acc;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) acc[m] = (ADD_I && h + 4 * m == c) ? 1.0 : 0.0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(at[t][s], b[t][s], acc, 0, 0, 0);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) d[t][m] = acc[m];
+  }
+}
+
+// Redefines x for the compiler (no instruction): broadcasts of x issued after a
+// pin cannot be hoisted above it.  Without the pins the scheduler computes every
+// row broadcast of a triangular loop up front -- NN(NN-1)/2 live doubles -- and
+// the kernel spills.
+template <int NN>
+__device__ __forceinline__ void pin(double (&x)[NN]) {
+#pragma unroll
+  for (int k = 0; k < NN; ++k) asm volatile("" : "+v"(x[k]));
+}
+__device__ __forceinline__ void pin(double& x) { asm volatile("" : "+v"(x)); }
+
+// lane i of each team: column i of the inverse of the lower-triangular J whose
+// rows the team holds (forward substitution J z = e_i), i.e. row i of J^-T
+template <int NN>
+__device__ __forceinline__ void team_tri_inverse_col(double (&jr)[NN], double& jrd,
+                                                     double (&z)[NN]) {
+  const int i = tlane();
+  sfor<0, NN>([&](auto R) {
+    constexpr int r = HD_K(R);
+    double t = i == r ? 1.0 : 0.0;
+    sfor<0, r>([&](auto K) { t = fma(-bc<r>(jr[HD_K(K)]), z[HD_K(K)], t); });
+    z[r] = t * bc<r>(jrd);
+    pin<NN>(jr);
+    pin(jrd);
+  });
+}
+
+// lane i of each team: (X x)_i for X's row i (xr) and x distributed over the team
+template <int NN>
+__device__ __forceinline__ double team_matvec(const double (&xr)[NN], double x) {
+  double y = 0.0;
+  sfor<0, NN>([&](auto K) { y = fma(xr[HD_K(K)], bc<HD_K(K)>(x), y); });
+  return y;
+}
+
+}  // namespace
+
+// ============================================================================
+// K1 (team, MFMA): per-(solve, layer) setup, four problems per wave
+// ============================================================================
+template <int NN>
+__global__ __launch_bounds__(64, 2) void hd_team_mfma_layer_kernel(LayerArgs A) {
+  __shared__ double lds[2 * kSet + 4 * 2 * 16];
+  double* S0 = lds;
+  double* S1 = lds + kSet;
+  double* G = lds + 2 * kSet;  // [t][dsq | gsq][16]
+  constexpr int N = 2 * NN;
+  const Quad<NN>& Qc = tquad<NN>(c_qt);
+  const int lane = (int)threadIdx.x;
+  const int h = lane >> 4, c = lane & 15;  // M layout
+  const int t = h, i = c;                  // T layout: team t, row i
+  const bool act = i < NN;
+  const int ii = act ? i : 0;
+  const int L = A.nlyr;
+  const long total = (long)A.nsc * L;
+  long team = (long)blockIdx.x * 4 + t;
+  // every lane takes part in the MFMA and LDS exchanges: a team past the end
+  // recomputes the last item and stores nothing
+  const bool valid = team < total;
+  if (!valid) team = total - 1;
+  // consecutive teams = consecutive solves of one layer -> contiguous records
+  const int sl = (int)(team % A.nsc);
+  const int lc = (int)(team / A.nsc);
+  const long s = A.s0 + sl;
+  const int nm = A.nmom;
+  const int np = A.nprop;
+  int st = 0;
+
+  // padding columns (>= NN) of both tile-sets are zero for the whole kernel
+  // except where a product's identity padding lands (block diagonal: harmless)
+  for (int k = lane; k < 2 * kSet; k += 64) lds[k] = 0.0;
+  lds_fence();
+
+  const double msk = act ? 1.0 : 0.0;
+  const double mu_i = fma(msk, Qc.mu[ii] - 1.0, 1.0);
+  const double sd_i = Qc.sd[ii] * msk;
+  const double g_i = Qc.g[ii] * msk;
+  const double rmu_i = Qc.rmu[ii] * msk;
+  const double rg_i = Qc.rg[ii] * msk;
+
+  // ---- inputs of this layer (harp layer L-1-lc) + delta-M (c_setdis) ----
+  const double* q = A.prop + ((size_t)s * L + (L - 1 - lc)) * np;
+  const double tau = q[0];
+  double ssa = np > 1 ? q[1] : 0.0;
+  if (!(tau >= 0.0) || !(ssa >= 0.0) || !(ssa <= 1.0)) st |= kStBadInput;
+  if (ssa == 1.0) ssa = 1.0 - kDither;
+  const double f = nm >= N ? q[1 + N] : 0.0;
+  if (!(f < 1.0)) st |= kStBadInput;
+  const double taup = (1.0 - ssa * f) * tau;
+  const double om = ssa * (1.0 - f) / (1.0 - ssa * f);
+  const double rf = om / (1.0 - f);
+
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
+  const double fb = A.fbeam ? A.fbeam[s] : 0.0;
+  const bool beam = fb > 0.0 && mu0 > 0.0;
+  if (beam && mu0 > 1.0) st |= kStBadInput;
+  const double rmu0 = beam ? 1.0 / mu0 : 0.0;
+  const double mub = beam ? mu0 : 0.0;
+
+  // ---- phase-matrix rows: S+ = -A+ (ap), S- = -A- (lch); beam source sums ----
+  double ap[NN], lch[NN];
+  double xs = 0.0, xd = 0.0;
+  sfor<0, NN>([&](auto J) { ap[HD_K(J)] = lch[HD_K(J)] = 0.0; });
+  {
+    double pprev = 0.0, pcur = 1.0;
+#pragma nounroll
+    for (int l2 = 0; l2 < NN; ++l2) {
+      const int le = 2 * l2, lo = le + 1;
+      const double che = le == 0 ? 1.0 : (le <= nm ? q[1 + le] : 0.0);
+      const double cho = lo <= nm ? q[1 + lo] : 0.0;
+      const double ge = (2 * le + 1) * (che - f) * rf;
+      const double go = (2 * lo + 1) * (cho - f) * rf;
+      const double pe0 = pcur;
+      const double po0 = ((2 * lo - 1) * mub * pcur - (lo - 1) * pprev) / lo;
+      pprev = po0;
+      pcur = ((2 * lo + 1) * mub * po0 - lo * pe0) / (lo + 1);
+      const double ue = ge * Qc.pt[le][ii] * msk;
+      const double uo = go * Qc.pt[lo][ii] * msk;
+      xs = fma(ue, pe0, xs);
+      xd = fma(uo, po0, xd);
+      sfor<0, NN>([&](auto J) {
+        constexpr int j = HD_K(J);
+        ap[j] = fma(ue, Qc.pt[le][j], ap[j]);
+        lch[j] = fma(uo, Qc.pt[lo][j], lch[j]);
+      });
+    }
+  }
+  sfor<0, NN>([&](auto J) {
+    constexpr int j = HD_K(J);
+    const double diag = i == j ? rmu_i : 0.0;
+    const double sij = sd_i * Qc.sd[j];
+    lch[j] = fma(-sij, lch[j], diag);
+    ap[j] = fma(-sij, ap[j], diag);
+  });
+  // L L^T = S-
+  double lt[NN], rdl;
+  if (!team_chol<NN, true>(lch, lt, rdl)) st |= kStEigen;
+
+  // ---- pre-Jacobi vectors (depend on L only) ----
+  double w2 = 0.0, lxd = 0.0;  // w2 = L^-T L^-1 g rv: V^T (L^-1 g rv) = U^T w2 later
+  const double fb2 = fb * (0.5 / kPi);
+  if (beam) {
+    const double y = sd_i * (fb2 * xs);
+    double z = 0.0;  // z = L^T y
+    sfor<0, NN>([&](auto K) { z = fma(lt[HD_K(K)], bc<HD_K(K)>(y), z); });
+    const double yl = team_matvec<NN>(lch, z);  // L z
+    const double xdi = -fb2 * xd;
+    const double rv = fma(-yl, rg_i, xdi * rmu0 * rmu_i);
+    w2 = g_i * rv;
+    lxd = sd_i * xdi;
+    team_lsolve<NN>(lch, rdl, w2);
+    team_usolve<NN>(lt, rdl, w2);
+    team_lsolve<NN>(lch, rdl, lxd);
+    team_usolve<NN>(lt, rdl, lxd);
+  }
+  double cvec = 0.0, db = 0.0, bsum = 0.0;
+  if (A.planck) {
+    const double bt = A.planckv[(size_t)(L - lc) * A.nsc + sl];
+    // a transparent layer carries its top level's Planck value through
+    // (c_disort's xr1 = 0 when dtaucpr = 0: B(tau) = xr0 = B_top)
+    const double bb = taup > 0.0 ? A.planckv[(size_t)(L - lc - 1) * A.nsc + sl] : bt;
+    db = bb - bt;
+    bsum = bt + bb;
+    const double b1 = taup > 0.0 ? 2.0 * db / taup : 0.0;
+    cvec = sd_i * mu_i;
+    team_lsolve<NN>(lch, rdl, cvec);
+    team_usolve<NN>(lt, rdl, cvec);
+    cvec = fma(b1 * rg_i, cvec, db) * msk;
+  }
+  {
+    double z[NN];
+    team_tri_inverse_col<NN>(lch, rdl, z);  // row i of L^-T -> S0 (lch dies here)
+    put_rows<NN>(S0, t, i, z);
+  }
+
+  // ---- C C^T = S+ ; B0 = C^T L (lane j: column j) ; C^-1 to LDS ----
+  double bcol[NN];
+  {
+    double unused[NN], rdc;
+    if (!team_chol<NN, false>(ap, unused, rdc)) st |= kStEigen;  // ap <- rows of C
+    sfor<0, NN>([&](auto I) {
+      constexpr int r = HD_K(I);
+      double u = 0.0;
+      sfor<r, NN>([&](auto K) { u = fma(bc<HD_K(K)>(ap[r]), lt[HD_K(K)], u); });
+      bcol[r] = u;
+      pin<NN>(ap);
+    });
+    double z[NN];
+    team_tri_inverse_col<NN>(ap, rdc, z);  // row i of C^-T -> S1
+    put_rows<NN>(S1, t, i, z);
+  }
+
+  // ---- eigenpairs (c_soleig): Sym = L^T S+ L = B0^T B0 = V diag(k^2) V^T ----
+  lds_fence();
+  team_jacobi<NN>(bcol, A.max_sweeps);  // B = B0 V, lane j: column j
+  lds_fence();
+  double kk;
+  {
+    double k2 = 0.0;
+    sfor<0, NN>([&](auto K) { k2 = fma(bcol[HD_K(K)], bcol[HD_K(K)], k2); });
+    if (act && !(k2 > 0.0)) st |= kStEigen;
+    kk = sqrt(k2 > 0.0 ? k2 : 0.0) * msk;
+    // Delta = tanh(k tau'/2)/k, Gamma = k tanh(k tau'/2) (lane j)
+    const double x = kk * taup;
+    const double m = -expm1(-x);
+    const double th = m * rcp_nr(2.0 - m);
+    const double delta = x > 1.0e-8 ? th * rcp_nr(kk > 0.0 ? kk : 1.0) : 0.5 * taup;
+    G[t * 32 + i] = sqrt(delta) * msk;
+    G[t * 32 + 16 + i] = sqrt(kk * th) * msk;
+  }
+
+  // ---- the dense products on the matrix core; vectors of the beam solution ----
+  // LDS holds what the next phase reads: S0 = L^-T rows, then W; S1 = C^-T rows,
+  // then B^T rows, then U^T (whose rows and columns feed the two beam matvecs)
+  double zp = 0.0, zm = 0.0, e0 = 0.0;
+  {
+    double X[4][4], Y[4][4], U[4][4], UT[4][4];
+    get_mt(S0, h, c, X);          // L^-1 (M)
+    mprod<false>(X, X, Y, h, c);  // W = L^-T L^-1
+    get_mt(S1, h, c, X);          // C^-1 (M)
+    lds_fence();
+    put_m(S0, h, c, Y);            // W, row-major
+    put_rows<NN>(S1, t, i, bcol);  // rows of B^T
+    lds_fence();
+    get_mt(S1, h, c, Y);           // B (M)
+    mprod<false>(X, Y, U, h, c);   // U = C^-T B
+    mprod<false>(Y, X, UT, h, c);  // U^T = B^T C^-1
+    lds_fence();
+    put_m(S1, h, c, UT);
+    lds_fence();
+    // beam (c_upbeam): tt = U^T w2 / (1/mu0^2 - k^2), sv = W^-1 D^1/2 U tt, then
+    // yy = W (sd mu sv) -- rows of U^T, columns of U^T, rows of W from LDS
+    if (beam) {
+      double r_[NN];
+      get_rows<NN>(S1, t, i, r_);
+      const double r2 = rmu0 * rmu0;
+      const double tv = team_matvec<NN>(r_, w2);
+      double den = fma(-kk, kk, r2);
+      if (act && fabs(den) < 1.0e-9 * r2) {
+        st |= kStResonance;
+        den = den < 0.0 ? -1.0e-9 * r2 : 1.0e-9 * r2;
+      }
+      const double ttv = tv / den * msk;
+      get_cols<NN>(S1, t, i, r_);
+      const double sv = team_matvec<NN>(r_, ttv) * rg_i;
+      get_rows<NN>(S0, t, i, r_);
+      const double yy = team_matvec<NN>(r_, sd_i * mu_i * sv);
+      const double tauc = A.tauc[(size_t)lc * A.nsc + sl];
+      const double att = 0.5 * exp(-tauc * rmu0);
+      const double dd = rg_i * fma(-yy, rmu0, lxd);
+      zp = (sv + dd) * att;
+      zm = (sv - dd) * att;
+      e0 = exp(-taup * rmu0);
+    }
+    get_m(S0, h, c, Y);            // W (M)
+    mprod<false>(U, Y, X, h, c);   // U^T W
+    // row scalings: Psi = Gamma^1/2 U^T W, Omega^T = Delta^1/2 U^T
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        X[tt][m] *= G[tt * 32 + 16 + h + 4 * m];
+        UT[tt][m] *= G[tt * 32 + h + 4 * m];
+      }
+    mprod<true>(UT, UT, U, h, c);  // I + Omega Omega^T
+    mprod<true>(X, X, Y, h, c);    // I + Psi^T Psi
+    lds_fence();
+    put_m(S0, h, c, U);
+    put_m(S1, h, c, Y);
+    lds_fence();
+  }
+  const double ga = g_i * (cvec - fma(-zp, e0, zm));
+  const double gb = g_i * (fma(zp, e0, zm) + bsum);
+
+  // ---- A- = (I + Omega Omega^T)^-1, A+ = (I + Psi^T Psi)^-1 ----
+  // J J^T = H (team Cholesky), K = J^-1 (team columns), A = K^T K (MFMA);
+  // Q~- ga = ga - A- ga, Q~+ gb = A+ gb - gb from the rows of A-, A+
+  double Am[4][4], Ap[4][4];
+  double pv, qv;
+  {
+    double hr[NN], unused[NN], z[NN], jrd, X[4][4];
+    get_rows<NN>(S0, t, i, hr);
+    if (!team_chol<NN, false>(hr, unused, jrd)) st |= kStEigen;
+    team_tri_inverse_col<NN>(hr, jrd, z);  // row i of K-^T
+    lds_fence();
+    put_rows<NN>(S0, t, i, z);
+    lds_fence();
+    get_mt(S0, h, c, X);
+    mprod<false>(X, X, Am, h, c);
+    lds_fence();
+    put_m(S0, h, c, Am);
+    lds_fence();
+    get_rows<NN>(S0, t, i, hr);
+    pv = ga - team_matvec<NN>(hr, ga);
+    get_rows<NN>(S1, t, i, hr);
+    if (!team_chol<NN, false>(hr, unused, jrd)) st |= kStEigen;
+    team_tri_inverse_col<NN>(hr, jrd, z);  // row i of K+^T
+    lds_fence();
+    put_rows<NN>(S1, t, i, z);
+    lds_fence();
+    get_mt(S1, h, c, X);
+    mprod<false>(X, X, Ap, h, c);
+    lds_fence();
+    put_m(S1, h, c, Ap);
+    lds_fence();
+    get_rows<NN>(S1, t, i, hr);
+    qv = team_matvec<NN>(hr, gb) - gb;
+  }
+
+  // ---- store: R~ = A+ - A-, T~ = A- + A+ - I (M layout), S~+, S~-, tau' (T) ----
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt) {
+    double chk = 0.0;
+    long tm = (long)blockIdx.x * 4 + tt;
+    const bool ok = tm < total;
+    if (!ok) tm = total - 1;
+    const int slt = (int)(tm % A.nsc), lct = (int)(tm / A.nsc);
+    double* rec = A.scr + ((size_t)lct * A.nsc + slt) * ne1t<NN>();
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int r = h + 4 * m;
+      const double rr = Ap[tt][m] - Am[tt][m];
+      const double tr = (Am[tt][m] + Ap[tt][m]) - (r == c ? 1.0 : 0.0);
+      if (ok && r < NN && c < NN) {
+        rec[r * NN + c] = rr;
+        rec[NN * NN + r * NN + c] = tr;
+      }
+      chk += rr + tr;
+    }
+    // this lane's share of problem tt's R~/T~: a non-finite entry flags problem tt
+    if (ok && !isfinite(chk)) {
+      atomicOr(&A.status[A.s0 + slt], kStNonFinite);
+      atomicOr(A.anyerr, 1);
+    }
+  }
+  double chk = 0.0;
+  const double sp = g_i * (zp * (1.0 - e0) - db) + pv - qv;
+  const double sm = g_i * (-zm * (1.0 - e0) + db) - pv - qv;
+  double* rec = A.scr + ((size_t)lc * A.nsc + sl) * ne1t<NN>();
+  if (valid && act) {
+    rec[2 * NN * NN + ii] = sp;
+    rec[2 * NN * NN + NN + ii] = sm;
+  }
+  chk += sp + sm;
+  if (valid && i == 0) rec[2 * NN * NN + 2 * NN] = taup;
+  if (act && !isfinite(chk + taup)) st |= kStNonFinite;
+  if (valid && st) {
+    atomicOr(&A.status[s], st);
+    if (st & 0x0F) atomicOr(A.anyerr, 1);
+  }
+}
+
+hipError_t upload_quad_tables_team_mfma(const QuadTablesTeam& t) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(c_qt), &t, sizeof(t), 0, hipMemcpyHostToDevice);
+}
+
+template <int NN>
+static hipError_t launch_layer(const LayerArgs& la, hipStream_t stream) {
+  const long nt1 = (long)la.nsc * la.nlyr;
+  const unsigned nb1 = (unsigned)((nt1 + 3) / 4);
+  hipLaunchKernelGGL(hd_team_mfma_layer_kernel<NN>, dim3(nb1), dim3(64), 0, stream, la);
+  return hipGetLastError();
+}
+
+hipError_t launch_team_layer_mfma(int nn, const LayerArgs& la, hipStream_t stream) {
+  switch (nn) {
+    case 9: return launch_layer<9>(la, stream);
+    case 10: return launch_layer<10>(la, stream);
+    case 11: return launch_layer<11>(la, stream);
+    case 12: return launch_layer<12>(la, stream);
+    case 13: return launch_layer<13>(la, stream);
+    case 14: return launch_layer<14>(la, stream);
+    case 15: return launch_layer<15>(la, stream);
+    case 16: return launch_layer<16>(la, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace hd
