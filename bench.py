@@ -12,8 +12,9 @@ nstr=16, nmom=16 (Henyey-Greenstein chi_l = g^l), nlyr=80, tau log-uniform
 1e3 columns x 64 g-points, nstr=32, nmom=32, nlyr=80, omega in [0.9, 0.9999],
 g in [0.6, 0.9] (delta-M active), umu0 in [0.1, 1].
 One step = one flux solve of every (g-point, column) pair of the rank's shard
-(hd_solve through the C-ABI) + the g-weighted band flux (C, L+1, 2),
-all-reduced over ranks.  Inputs are generated on the device before the timed
++ the g-weighted band flux (C, L+1, 2) -- fused into the solve
+(hd_solve_band: the per-g fluxes are never stored; ``--no-fuse`` = hd_solve
+writing them + hd_band_flux) -- all-reduced over ranks.  Inputs are generated on the device before the timed
 region (seeded per g-point, so the global problem does not depend on N).
 Spectral sharding: rank r owns g-points {g : g mod N == r} (fixed global
 problem -> "scaling": "strong").
@@ -257,6 +258,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--chunk", type=int, default=0,
                     help="max solves per internal chunk (hd_context_set_chunk; 0 = auto)")
+    ap.add_argument("--no-fuse", action="store_true",
+                    help="unfused epilogue: per-g fluxes stored by hd_solve, then hd_band_flux")
     ap.add_argument("--graph", action="store_true",
                     help="replay the solve + band sum as one captured HIP graph per step")
     args = ap.parse_args()
@@ -309,14 +312,18 @@ def main():
         op.wave_lower(list(wl)).wave_upper(list(wu))
     op.ds().nlyr, op.ds().nstr, op.ds().nmom = nlyr, nstr, nstr
     disort = Disort(op)
-    flux = torch.empty((W, ncol, nlyr + 1, 2), dtype=torch.float64, device=dev)
+    fuse = not args.no_fuse
+    flux = None if fuse else torch.empty((W, ncol, nlyr + 1, 2), dtype=torch.float64, device=dev)
     status = torch.zeros(W * ncol, dtype=torch.int32, device=dev)
 
     band = torch.empty((ncol, nlyr + 1, 2), dtype=torch.float64, device=dev)
 
     def solve():
-        disort.forward(prop, bc, temf, status=status, out=flux)
-        band_flux(flux, wts, out=band)
+        if fuse:
+            disort.forward_band(prop, bc, temf, weights=wts, out=band, status=status)
+        else:
+            disort.forward(prop, bc, temf, status=status, out=flux)
+            band_flux(flux, wts, out=band)
 
     if args.chunk:
         _context(dev_index).set_chunk(args.chunk)
@@ -425,6 +432,16 @@ def main():
                  "timing": timing_note}
         cpu = None
         max_err = None
+        fused_vs_unfused = None
+        if fuse and world == 1:
+            # per-g fluxes (untimed) for the parity checks; the fused band against
+            # hd_band_flux over them (only the summation order differs)
+            band_fused = band.clone()
+            flux = torch.empty((W, ncol, nlyr + 1, 2), dtype=torch.float64, device=dev)
+            disort.forward(prop, bc, temf, status=status, out=flux)
+            bunf = band_flux(flux, wts)
+            fused_vs_unfused = float(((band_fused - bunf).abs().max() /
+                                      bunf.abs().max()).item())
         if world == 1 and not args.no_cpu_baseline:
             cpu, ref, n = cpu_baseline(prop, bc, temf, nstr, args.planck, wl, wu)
             m = ref.shape[0]
@@ -442,11 +459,15 @@ def main():
                        "nmom": nstr, "nlyr": nlyr, "planck": bool(args.planck),
                        "parallelism": f"spectral g mod {world}",
                        "hip_graph": bool(args.graph), "chunk": args.chunk or "auto",
+                       "epilogue": ("band sum fused into the solve (hd_solve_band; per-g "
+                                    "fluxes not stored)" if fuse else
+                                    "per-g fluxes stored (hd_solve) + hd_band_flux"),
                        "collective": ("all_reduce of the g-weighted band flux (" +
                                       ("gloo, rehearsal" if rehearse else "RCCL") + ")") if world > 1
                        else "none"},
             "roofline": roofline, "path_roofline": whole, "cpu_baseline": cpu,
             "max_rel_err_vs_cpu_restatement": max_err,
+            "band_fused_vs_unfused_max_rel": fused_vs_unfused,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -123,6 +123,34 @@ int hd_solve(hd_context *ctx, const hd_config *cfg, const hd_inputs *in, double 
              int *status, void *stream);
 
 /*
+ * Fused band epilogue: the solve of hd_solve plus the
+ * weighted sum over the wave axis that every harp caller applies next --
+ *   bflux[c][lev][dir] = sum_w weight[w] flux[w][c][lev][dir]
+ * (examples/amars_lw.cpp:84-88 `(flux * weights.view({-1,1,1,1})).sum(0)`,
+ * examples/amars_sw.cpp:169-196 with weight = d(wavenumber); legacy
+ * src/rtsolver/rt_solver_disort.cpp_:183-184).  For nstr <= 16 the sum is
+ * formed in the back-substitution epilogue (solves taken column by column,
+ * the weighted fluxes of a column summed across lanes), so the per-point
+ * fluxes never reach memory; for nstr 18..32 each chunk's fluxes are summed
+ * into bflux after the chunk.  The summation order is fixed (deterministic
+ * for a given shape and chunk size; no atomics).  Heating rates and the
+ * spherical correction follow from bflux (hdharp.h) -- after the cross-rank
+ * all-reduce when a band's points are sharded over GPUs.
+ *   band->weight  DEVICE [nwave]
+ *   band->bflux   DEVICE [ncol][nlyr+1][2], overwritten
+ *   flux          DEVICE [nwave][ncol][nlyr+1][2] or NULL (per-point fluxes
+ *                 are then not stored)
+ * status / stream / return codes as hd_solve.
+ */
+typedef struct hd_band {
+  const double *weight;
+  double *bflux;
+} hd_band;
+
+int hd_solve_band(hd_context *ctx, const hd_config *cfg, const hd_inputs *in,
+                  const hd_band *band, double *flux, int *status, void *stream);
+
+/*
  * Intensity path (flags usrtau / usrang, onlyfl off): pydisort's forward with
  * radiances and DisortImpl::get_rad [EXTERNAL], as called at
  * tests/test_disort.cpp:13-55 (user_mu, user_phi, user_tau; get_rad at :52)

@@ -25,7 +25,8 @@ HD_STATUS_ERROR_MASK = 0x0F
 # every symbol include/hdisort.h declares
 EXPORTED = ("hd_version", "hd_last_error", "hd_context_create", "hd_context_destroy",
             "hd_context_set_chunk", "hd_context_set_timing", "hd_context_get_timing",
-            "hd_context_reserve", "hd_solve", "hd_solve_radiance", "hd_quadrature")
+            "hd_context_reserve", "hd_solve", "hd_solve_band", "hd_solve_radiance",
+            "hd_quadrature")
 
 # every symbol include/hdharp.h declares (harp-side steps around the solve)
 HARP_EXPORTED = ("hd_attenuate", "hd_band_optics", "hd_rfm_attenuate", "hd_band_flux",
@@ -64,6 +65,10 @@ class HdRadiance(ctypes.Structure):
                 ("corint", ctypes.c_int)]
 
 
+class HdBand(ctypes.Structure):
+    _fields_ = [("weight", _dp), ("bflux", _dp)]
+
+
 class HdTiming(ctypes.Structure):
     _fields_ = [("layer_ms", ctypes.c_double), ("sweep_ms", ctypes.c_double),
                 ("layer_launches", ctypes.c_int), ("sweep_launches", ctypes.c_int)]
@@ -96,6 +101,9 @@ def load(path: str = LIB_PATH):
     lib.hd_context_reserve.argtypes = [ctypes.c_void_p, ctypes.POINTER(HdConfig), ctypes.c_long]
     lib.hd_solve.argtypes = [ctypes.c_void_p, ctypes.POINTER(HdConfig), ctypes.POINTER(HdInputs),
                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.hd_solve_band.argtypes = [ctypes.c_void_p, ctypes.POINTER(HdConfig),
+                                  ctypes.POINTER(HdInputs), ctypes.POINTER(HdBand),
+                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.hd_solve_radiance.argtypes = [ctypes.c_void_p, ctypes.POINTER(HdConfig),
                                       ctypes.POINTER(HdInputs), ctypes.POINTER(HdRadiance),
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -167,6 +175,14 @@ class Context:
         rc = load().hd_solve(self.handle, ctypes.byref(cfg), ctypes.byref(inp),
                              ctypes.c_void_p(flux_ptr), ctypes.c_void_p(status_ptr or 0),
                              ctypes.c_void_p(stream_ptr or 0))
+        check(rc, self.handle)
+
+    def solve_band(self, cfg: HdConfig, inp: HdInputs, band: HdBand, flux_ptr: int | None,
+                   status_ptr: int | None, stream_ptr: int | None):
+        rc = load().hd_solve_band(self.handle, ctypes.byref(cfg), ctypes.byref(inp),
+                                  ctypes.byref(band), ctypes.c_void_p(flux_ptr or 0),
+                                  ctypes.c_void_p(status_ptr or 0),
+                                  ctypes.c_void_p(stream_ptr or 0))
         check(rc, self.handle)
 
     def solve_radiance(self, cfg: HdConfig, inp: HdInputs, rad: HdRadiance, flux_ptr: int,

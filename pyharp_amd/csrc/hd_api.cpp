@@ -413,19 +413,29 @@ namespace {
 // hd_solve's enqueue body: everything it launches ends on `stream` (the side
 // and lay streams fork from it and join back into it)
 int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double* flux,
-                  int*& status, hipStream_t stream) {
+                  const hd_band* band, int*& status, hipStream_t stream) {
   int rc = HD_OK;
   const long nsolve = (long)in->nwave * in->ncol;
   const int nn = cfg->nstr / 2;
   const int nlyr = cfg->nlyr;
   const bool planck = (cfg->flags & HD_FLAG_PLANCK) != 0;
   const bool sync = status == nullptr;
+  const bool reg = nn <= hd::kMaxRegNN;
+  const size_t nlev2 = 2 * (size_t)(nlyr + 1);
 
   long chunk = ctx->chunk > 0 ? std::min(ctx->chunk, nsolve) : auto_chunk(nsolve, nn, nlyr, planck);
   const size_t ne1 = hd::layer_record_doubles(nn);
   const size_t ne2 = hd::bsub_record_doubles(nn);
   const size_t per = hd::scratch_doubles_per_solve(nn, nlyr, planck);
-  rc = ensure_scratch(ctx, per * chunk);
+  // fused band epilogue: register path -- column-major chunks, the surface
+  // fluxes of two chunks in flight [2][2][chunk] and one chunk's run partials
+  // [wave][nslot][lev][2]; team path -- one chunk's fluxes when the caller
+  // keeps none
+  const int nslot = band ? hd::band_slots(in->nwave) : 0;
+  size_t band_extra = 0;
+  if (band && reg) band_extra = 4 * (size_t)chunk + (size_t)((chunk + 63) / 64) * nslot * nlev2;
+  if (band && !reg && !flux) band_extra = (size_t)chunk * nlev2;
+  rc = ensure_scratch(ctx, per * chunk + band_extra);
   if (rc) return rc;
   rc = ensure_tables(ctx);
   if (rc) return rc;
@@ -437,8 +447,8 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
   HD_HIP(ctx, hipMemsetAsync(status, 0, sizeof(int) * nsolve, stream));
   HD_HIP(ctx, hipMemsetAsync(ctx->anyerr, 0, sizeof(int), stream));
   const int nm = std::max(0, std::min(cfg->nmom, cfg->nprop - 2));
+  const int cmaj = band && reg ? 1 : 0;
 
-  const bool reg = nn <= hd::kMaxRegNN;
   // a register-path call of one chunk has nothing to overlap: it runs wholly on
   // the caller's stream (prologue, layer kernel, sweep, tail back-substitution),
   // without the fork/join of the three-stream pipeline below (C1/C3 latency)
@@ -457,6 +467,7 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
   double* xsurf_b[2];
   double* planck_b[2];
   double* tauc_b[2];
+  double* band_q = nullptr;  // band-epilogue scratch after the regions
   {
     double* q = ctx->scratch;
     for (int b = 0; b < nb; ++b, q += ne1 * nlyr * (size_t)chunk) layer_b[b] = q;
@@ -467,7 +478,32 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
       if (planck) q += (size_t)(nlyr + 3) * chunk;
     }
     for (int b = 0; b < nb; ++b, q += (size_t)nlyr * chunk) tauc_b[b] = q;
+    band_q = q;
   }
+  double* fsurf_b[2] = {nullptr, nullptr};
+  double* part = nullptr;
+  double* fchunk = nullptr;
+  if (band && reg) {
+    fsurf_b[0] = band_q;
+    fsurf_b[1] = band_q + 2 * (size_t)chunk;
+    part = band_q + 4 * (size_t)chunk;
+  } else if (band) {
+    fchunk = flux ? nullptr : band_q;
+  }
+  auto band_args = [&](long s0, int nsc) {
+    hd::BandArgs ba{};
+    ba.part = part;
+    ba.fchunk = part ? nullptr : (flux ? flux + (size_t)s0 * nlev2 : fchunk);
+    ba.wts = band->weight;
+    ba.bflux = band->bflux;
+    ba.s0 = s0;
+    ba.nsc = nsc;
+    ba.ncol = in->ncol;
+    ba.nwave = in->nwave;
+    ba.nlev = nlyr + 1;
+    ba.nslot = nslot;
+    return ba;
+  };
   auto prologue_args = [&](long s0, int nsc, int b, hd::TaucArgs& ta, hd::PlanckArgs& pa) {
     ta = hd::TaucArgs{};
     ta.prop = in->prop;
@@ -478,6 +514,9 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
     ta.nprop = cfg->nprop;
     ta.use_f = nm >= cfg->nstr;
     ta.f_slot = 1 + cfg->nstr;
+    ta.cmaj = cmaj;
+    ta.nwave = in->nwave;
+    ta.ncol = in->ncol;
     pa = hd::PlanckArgs{};
     pa.temf = in->temf;
     pa.btemp = in->btemp;
@@ -490,6 +529,8 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
     pa.nsc = nsc;
     pa.ncol = in->ncol;
     pa.nlyr = nlyr;
+    pa.cmaj = cmaj;
+    pa.nwave = in->nwave;
   };
 
   if (reg && !single) {
@@ -530,6 +571,8 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
     la.planck = planck;
     la.max_sweeps = 16;
     la.sink = ctx->sink;
+    la.cmaj = cmaj;
+    la.nwave = in->nwave;
     hd::SweepArgs sa{};
     sa.scr = layer_b[buf];
     sa.bsub = bsub_b[buf];
@@ -548,6 +591,18 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
     sa.nlyr = nlyr;
     sa.planck = planck;
     sa.sink = ctx->sink;
+    sa.cmaj = cmaj;
+    sa.nwave = in->nwave;
+    if (band && reg) {
+      sa.wts = band->weight;
+      sa.part = part;
+      sa.fsurf = fsurf_b[buf];
+      sa.nslot = nslot;
+      sa.rsteps = hd::band_steps(in->nwave);
+    } else if (band && !flux) {
+      sa.flux = fchunk;
+      sa.flux_local = 1;
+    }
     hipEvent_t* ev = nullptr;
     if (ctx->timing) {
       if (ctx->pool_used >= 4 * 512) {
@@ -571,6 +626,7 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
       if (e == hipSuccess) e = hd::launch_sweep_nn(nn, sa, stream);
       if (ev) HD_HIP(ctx, hipEventRecord(ev[3], stream));
       if (e == hipSuccess) e = hd::launch_backsub_nn(nn, sa, stream, true);
+      if (e == hipSuccess && band) e = hd::launch_band_reduce(band_args(s0, nsc), stream);
     } else if (reg) {
       // layer kernel k on `lay`: its inputs (prologue k) are in, and sweep k-2,
       // the last reader of layer records[buf], is done
@@ -591,6 +647,7 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
       }
     } else {
       e = hd::launch_solve_chunk_team(nn, nullptr, nullptr, la, sa, stream, ev);
+      if (e == hipSuccess && band) e = hd::launch_band_reduce(band_args(s0, nsc), stream);
     }
     if (e != hipSuccess) return fail(ctx, HD_EHIP, "hd_solve: launch failed: %s", hipGetErrorString(e));
     if (reg && !single) {
@@ -607,6 +664,7 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
       }
       HD_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_sweep[buf], 0));
       e = hd::launch_backsub_nn(nn, sa, ctx->side, s1 >= nsolve);  // last chunk: tail kernel
+      if (e == hipSuccess && band) e = hd::launch_band_reduce(band_args(s0, nsc), ctx->side);
       if (e != hipSuccess)
         return fail(ctx, HD_EHIP, "hd_solve: back-substitution launch failed: %s",
                     hipGetErrorString(e));
@@ -663,7 +721,22 @@ int hd_solve(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double*
   if (rc) return rc;
   if ((long)in->nwave * in->ncol == 0) return HD_OK;
   return run_solve(ctx, status, stream, "hd_solve", [&](int*& st, hipStream_t s) {
-    return solve_enqueue(ctx, cfg, in, flux, st, s);
+    return solve_enqueue(ctx, cfg, in, flux, nullptr, st, s);
+  });
+}
+
+int hd_solve_band(hd_context* ctx, const hd_config* cfg, const hd_inputs* in,
+                  const hd_band* band, double* flux, int* status, void* stream) {
+  if (!ctx) return fail(nullptr, HD_EINVAL, "hd_solve_band: null context");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!band || !band->weight || !band->bflux)
+    return fail(ctx, HD_EINVAL, "hd_solve_band: band weights and bflux are required");
+  // flux is optional here: validate against a non-null stand-in
+  int rc = validate(ctx, cfg, in, flux ? flux : band->bflux);
+  if (rc) return rc;
+  if ((long)in->nwave * in->ncol == 0) return HD_OK;
+  return run_solve(ctx, status, stream, "hd_solve_band", [&](int*& st, hipStream_t s) {
+    return solve_enqueue(ctx, cfg, in, flux, band, st, s);
   });
 }
 

@@ -66,7 +66,7 @@ __global__ __launch_bounds__(256) void hd_planck_kernel(PlanckArgs A) {
   if (tid >= (long)A.nsc * nl) return;
   const int lev = (int)(tid / A.nsc);
   const int sl = (int)(tid - (long)lev * A.nsc);
-  const long s = A.s0 + sl;
+  const long s = solve_of(A.s0 + sl, A.cmaj, A.nwave, A.ncol);
   const int w = (int)(s / A.ncol);
   const int c = (int)(s - (long)w * A.ncol);
   double b;
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256) void hd_planck_kernel(PlanckArgs A) {
 __global__ __launch_bounds__(256) void hd_tauc_kernel(TaucArgs A) {
   const long sl = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (sl >= A.nsc) return;
-  const long s = A.s0 + sl;
+  const long s = solve_of(A.s0 + sl, A.cmaj, A.nwave, A.ncol);
   const int L = A.nlyr, np = A.nprop;
   const double* p = A.prop + (size_t)s * L * np;
   double tauc = 0.0;
@@ -122,7 +122,7 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
   const int lc = tl * kLayersPerBlock + (lt >> 6);  // solver layer, 0 = top
   const int L = A.nlyr;
   if (sl >= A.nsc || lc >= L) return;
-  const long s = A.s0 + sl;
+  const long s = solve_of(A.s0 + sl, A.cmaj, A.nwave, A.ncol);
   const int nm = A.nmom;
   const int np = A.nprop;
   int st = 0;
@@ -507,7 +507,7 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
   const Quad<NN>& Qc = quad<NN>();
   const long sl = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (sl >= A.nsc) return;
-  const long s = A.s0 + sl;
+  const long s = solve_of(A.s0 + sl, A.cmaj, A.nwave, A.ncol);
   const int L = A.nlyr;
   const size_t nsc = A.nsc;
   constexpr int nsym = NN * (NN + 1) / 2;
@@ -721,7 +721,6 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
   double ip[NN];
 #pragma unroll
   for (int i = 0; i < NN; ++i) ip[i] = Qc.g[i] * x;
-  double* fo = A.flux + (size_t)s * (L + 1) * 2;
   double chk = 0.0;
   {
     double up = 0.0, dn = 0.0;
@@ -733,9 +732,17 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
       for (int j = 0; j < NN; ++j) t += HD_SYM(ra, i, j) * ip[j];
       dn += Qc.g[i] * t;
     }
-    fo[0] = twopi * up;
-    fo[1] = twopi * dn + dirsurf;
-    chk += fo[0] + fo[1];
+    const double f0 = twopi * up, f1 = twopi * dn + dirsurf;
+    if (A.flux) {
+      double* fo = A.flux + (size_t)s * (L + 1) * 2;
+      fo[0] = f0;
+      fo[1] = f1;
+    }
+    if (A.fsurf) {  // band epilogue: the back-substitution sums the surface level too
+      A.fsurf[sl] = f0;
+      A.fsurf[nsc + sl] = f1;
+    }
+    chk += f0 + f1;
   }
   A.xsurf[sl] = x;
   if (!isfinite(chk)) st |= kStNonFinite;
@@ -757,9 +764,14 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
 template <int NN, bool PRE>
 __device__ __forceinline__ void backsub_body(const SweepArgs& A) {
   const Quad<NN>& Qc = quad<NN>();
-  const long sl = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (sl >= A.nsc) return;
-  const long s = A.s0 + sl;
+  const long lane_sl = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = lane_sl < A.nsc;
+  const bool band = A.part != nullptr;
+  // with the band epilogue every lane of a wave takes part in the cross-lane
+  // sums: lanes past the chunk run on the last solve's records with weight 0
+  if (!live && !band) return;
+  const long sl = live ? lane_sl : A.nsc - 1;
+  const long s = solve_of(A.s0 + sl, A.cmaj, A.nwave, A.ncol);
   const int L = A.nlyr;
   const size_t nsc = A.nsc;
   const double twopi = 2.0 * kPi;
@@ -767,8 +779,55 @@ __device__ __forceinline__ void backsub_body(const SweepArgs& A) {
   double ip[NN];
 #pragma unroll
   for (int i = 0; i < NN; ++i) ip[i] = Qc.g[i] * x;
-  double* fo = A.flux + (size_t)s * (L + 1) * 2;
+  double* fo = A.flux ? A.flux + (size_t)s * (L + 1) * 2 : nullptr;
   double chk = 0.0;
+  // band epilogue (cmaj order, q = col*nwave + w): lanes of one column form a
+  // run; Hillis-Steele suffix sums inside the run leave the run's total (fixed
+  // association order) in its first lane, which stores the wave's partial
+  double wgt = 0.0;
+  unsigned same = 0;  // bit k: lane + 2^k is in this lane's run
+  bool head = false;
+  double* pp = nullptr;
+  if (band) {
+    const long q = A.s0 + lane_sl;
+    const long col = q / A.nwave;
+    const int lane = (int)(lane_sl & 63);
+    wgt = live ? A.wts[q - col * A.nwave] : 0.0;
+    for (int k = 0; k < A.rsteps; ++k) {
+      const int d = 1 << k;
+      const long oc = __shfl_down(col, d);
+      if (lane + d < 64 && oc == col) same |= 1u << k;
+    }
+    head = live && (lane == 0 || q % A.nwave == 0);
+    const long wv = lane_sl >> 6;
+    const long cfirst = (A.s0 + (wv << 6)) / A.nwave;
+    pp = A.part + ((size_t)wv * A.nslot + (size_t)(col - cfirst)) * (L + 1) * 2;
+  }
+  auto emit = [&](int lev, double up, double dn, bool write_flux) {
+    if (write_flux && fo && live) {
+      fo[2 * lev] = up;
+      fo[2 * lev + 1] = dn;
+    }
+    if (band) {
+      double a = wgt * up, b = wgt * dn;
+      for (int k = 0; k < A.rsteps; ++k) {
+        const double a2 = __shfl_down(a, 1 << k);
+        const double b2 = __shfl_down(b, 1 << k);
+        if (same & (1u << k)) {
+          a += a2;
+          b += b2;
+        }
+      }
+      if (head) {
+        pp[2 * lev] = a;
+        pp[2 * lev + 1] = b;
+      }
+    }
+  };
+  if (band) {  // surface level, from the sweep
+    const double f0 = A.fsurf[sl], f1 = A.fsurf[nsc + sl];
+    emit(0, f0, f1, false);
+  }
   // element e of this layer's record (e = i NN + j: ZT; NN^2 + i: t;
   // NN^2 + NN + i: rc; NN^2 + 2 NN: cs) through `get`
   auto layer = [&](int lc, auto&& get) {
@@ -788,9 +847,8 @@ __device__ __forceinline__ void backsub_body(const SweepArgs& A) {
       dn += get(NN * NN + NN + i) * nip[i];
     }
     const int lev = L - lc;
-    fo[2 * lev] = twopi * up;
-    fo[2 * lev + 1] = dn;
-    chk += fo[2 * lev] + fo[2 * lev + 1];
+    emit(lev, twopi * up, dn, true);
+    chk += twopi * up + dn;
   };
   auto rec_ptr = [&](int lc) { return A.bsub + (size_t)lc * ne2<NN>() * nsc + sl; };
   if constexpr (PRE) {
@@ -817,7 +875,7 @@ __device__ __forceinline__ void backsub_body(const SweepArgs& A) {
       layer(lc, [&](int e) { return bp[e * nsc]; });
     }
   }
-  if (!isfinite(chk)) {
+  if (live && !isfinite(chk)) {
     atomicOr(&A.status[s], kStNonFinite);
     atomicOr(A.anyerr, 1);
   }
@@ -842,6 +900,58 @@ void hd_backsub_kernel(SweepArgs A) {
 template <int NN>
 __global__ __launch_bounds__(64) void hd_backsub_tail_kernel(SweepArgs A) {
   backsub_body<NN, true>(A);
+}
+
+// ============================================================================
+// K4: fused band epilogue of one chunk (hd_solve_band), per (column, level,
+// direction): bflux[c] = (first chunk of c ? 0 : bflux[c]) + the chunk's part,
+// summed in wave-point order -- deterministic, no atomics
+// ============================================================================
+__global__ __launch_bounds__(256) void hd_band_reduce_kernel(BandArgs B) {
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int per = 2 * B.nlev;
+  const long W = B.nwave;
+  const long q0 = B.s0, q1 = B.s0 + B.nsc;
+  if (B.part) {  // register path, column-major chunk: the waves' run partials
+    const long c = q0 / W + tid / per;
+    if (c > (q1 - 1) / W) return;
+    const int e = (int)(tid % per);
+    const long qa = c * W > q0 ? c * W : q0;
+    const long qb = ((c + 1) * W < q1 ? (c + 1) * W : q1) - 1;
+    double sum = 0.0;
+    for (long wv = (qa - q0) >> 6; wv <= (qb - q0) >> 6; ++wv) {
+      const long cf = (q0 + (wv << 6)) / W;
+      sum += B.part[((size_t)wv * B.nslot + (size_t)(c - cf)) * per + e];
+    }
+    double* o = B.bflux + (size_t)c * per + e;
+    *o = c * W >= q0 ? sum : *o + sum;
+  } else {  // team path: the chunk's fluxes, solves s = w*ncol + c in [s0, s1)
+    const long c = tid / per;
+    if (c >= B.ncol) return;
+    const int e = (int)(tid % per);
+    const long wa = q0 <= c ? 0 : (q0 - c + B.ncol - 1) / B.ncol;
+    if (q1 - 1 < c) return;
+    long wb = (q1 - 1 - c) / B.ncol;
+    if (wb > W - 1) wb = W - 1;
+    if (wa > wb) return;
+    double sum = 0.0;
+    for (long w = wa; w <= wb; ++w)
+      sum += B.wts[w] * B.fchunk[(size_t)(w * B.ncol + c - q0) * per + e];
+    double* o = B.bflux + (size_t)c * per + e;
+    *o = wa == 0 ? sum : *o + sum;
+  }
+}
+
+hipError_t launch_band_reduce(const BandArgs& ba, hipStream_t stream) {
+  long n;
+  if (ba.part) {
+    n = ((ba.s0 + ba.nsc - 1) / ba.nwave - ba.s0 / ba.nwave + 1) * 2L * ba.nlev;
+  } else {
+    n = (long)ba.ncol * 2 * ba.nlev;
+  }
+  hipLaunchKernelGGL(hd_band_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     stream, ba);
+  return hipGetLastError();
 }
 
 // ============================================================================

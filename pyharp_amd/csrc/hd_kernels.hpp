@@ -25,6 +25,18 @@ __host__ __device__ constexpr int sym_index(int i, int j) {
   return i <= j ? i * NN - i * (i - 1) / 2 + (j - i) : j * NN - j * (j - 1) / 2 + (i - j);
 }
 
+// Chunk lane -> solve.  A call's solves are processed in chunks of consecutive
+// indices q = s0 + sl.  Normally q is the caller's solve s = wave*ncol + col;
+// with the fused band epilogue (hd_solve_band) the order is column-major,
+// q = col*nwave + wave, so that the wave-points of one column sit in
+// neighbouring lanes and their weighted fluxes are summed across lanes.
+// (32-bit arithmetic: hd_solve limits nwave*ncol to 2^31 - 1)
+__host__ __device__ inline long solve_of(long q, int cmaj, int nwave, int ncol) {
+  if (!cmaj) return q;
+  const unsigned qu = (unsigned)q, c = qu / (unsigned)nwave;
+  return (long)(qu - c * (unsigned)nwave) * ncol + c;
+}
+
 struct PlanckArgs {
   const double* temf;   // [ncol][nlyr+1], level 0 = bottom
   const double* btemp;  // [S] or null
@@ -37,6 +49,8 @@ struct PlanckArgs {
   int nsc;
   int ncol;
   int nlyr;
+  int cmaj;   // column-major chunk order (solve_of)
+  int nwave;
 };
 
 struct TaucArgs {
@@ -48,6 +62,9 @@ struct TaucArgs {
   int nprop;
   int use_f;    // delta-M active (moments >= nstr available)
   int f_slot;   // prop slot of chi_nstr = 1 + nstr
+  int cmaj;     // column-major chunk order (solve_of)
+  int nwave;
+  int ncol;
 };
 
 struct LayerArgs {
@@ -68,6 +85,8 @@ struct LayerArgs {
   int planck;
   int max_sweeps;
   double* sink;  // team path: store target of lanes >= NN (>= 2*16^2+2*16+2 doubles)
+  int cmaj;      // column-major chunk order (solve_of)
+  int nwave;
 };
 
 struct SweepArgs {
@@ -88,6 +107,34 @@ struct SweepArgs {
   int nlyr;
   int planck;
   double* sink;  // team path: store target of lanes >= NN
+  int cmaj;      // column-major chunk order (solve_of)
+  int nwave;
+  // fused band epilogue (hd_solve_band); part == nullptr: off.  Register path:
+  // the back-substitution sums wts[w] F over the lanes of a column (segmented,
+  // fixed order) and a wave's segment heads store [wave][slot][lev][2] partials;
+  // fsurf [2][nsc] carries the sweep's surface fluxes to it.  flux may then be null.
+  const double* wts;
+  double* part;
+  double* fsurf;
+  int nslot;       // column slots per wave
+  int rsteps;      // ceil(log2(min(nwave, 64))) shuffle steps
+  int flux_local;  // team path: flux is a chunk buffer [nsc][L+1][2]
+};
+
+// chunk epilogue of the fused band sum: bflux[c] (=|+=) sum of the chunk's
+// partials of column c, in wave order (cmaj: register-path partials; else the
+// chunk flux buffer of the team path in wave-point order)
+struct BandArgs {
+  const double* part;   // register path: [wave][nslot][nlev][2]
+  const double* fchunk; // team path: [nsc][nlev][2]
+  const double* wts;    // [nwave]
+  double* bflux;        // [ncol][nlev][2]
+  long s0;
+  int nsc;
+  int ncol;
+  int nwave;
+  int nlev;
+  int nslot;
 };
 
 struct QuadHost {
@@ -113,6 +160,15 @@ hipError_t launch_solve_chunk_team(int nn, const PlanckArgs* pa, const TaucArgs*
                                    const LayerArgs& la, const SweepArgs& sa, hipStream_t stream,
                                    hipEvent_t* ev);
 size_t scratch_doubles_per_solve(int nn, int nlyr, bool planck);
+// the chunk epilogue of hd_solve_band (after the chunk's back-substitution)
+hipError_t launch_band_reduce(const BandArgs& ba, hipStream_t stream);
+// column slots a 64-lane wave of consecutive column-major solves can touch
+inline int band_slots(int nwave) { return nwave >= 64 ? 2 : (63 / nwave + 2 < 64 ? 63 / nwave + 2 : 64); }
+inline int band_steps(int nwave) {
+  int k = 0;
+  while ((1 << k) < (nwave < 64 ? nwave : 64)) ++k;
+  return k;
+}
 // record an error for hd_last_error(NULL) (entry points without a context); returns code
 int set_global_error(int code, const char* fmt, ...);
 // doubles per (layer, solve) of the layer-operator and back-substitution records

@@ -500,7 +500,8 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_sweep_kernel(SweepArgs A) 
   if (beam) esurf += alb * dirsurf / kPi;
   const double x = (2.0 * alb * gsd + esurf) / (1.0 - 2.0 * alb * grg);
   double ip = g_i * x;
-  double* fo = A.flux + (size_t)s * (L + 1) * 2;
+  // flux_local: the band epilogue's chunk buffer (hd_solve_band without per-point fluxes)
+  double* fo = A.flux + (size_t)(A.flux_local ? (long)sl : s) * (L + 1) * 2;
   double chk = 0.0;
   {
     const double up = team_sum(g_i * ip);

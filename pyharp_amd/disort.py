@@ -199,6 +199,24 @@ class Disort(RTSolver):
     def forward(self, prop: torch.Tensor, bc: Optional[Dict[str, torch.Tensor]] = None,
                 temf: Optional[torch.Tensor] = None, *, status: Optional[torch.Tensor] = None,
                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        return self._forward(prop, bc, temf, status=status, out=out)
+
+    def forward_band(self, prop: torch.Tensor, bc: Optional[Dict[str, torch.Tensor]] = None,
+                     temf: Optional[torch.Tensor] = None, *, weights: torch.Tensor,
+                     out: Optional[torch.Tensor] = None, flux: Optional[torch.Tensor] = None,
+                     status: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """The band flux (ncol, nlyr+1, 2) = sum_w weights[w] F_w of this batch, with
+        the sum fused into the solve (hd_solve_band): what every harp caller does
+        with forward's result next (examples/amars_lw.cpp:84-88
+        ``(flux * weights.view({-1,1,1,1})).sum(0)``; amars_sw.cpp:169-196 with
+        weights = d(wavenumber)).  Per-point fluxes are stored only if ``flux``
+        (nwave, ncol, nlyr+1, 2) is given.  Fixed summation order, no atomics."""
+        if self.radiance:
+            raise RuntimeError("Disort.forward_band: the fused band sum is a flux-only path "
+                               "(onlyfl without usrtau)")
+        return self._forward(prop, bc, temf, status=status, out=flux, band=(weights, out))
+
+    def _forward(self, prop, bc, temf, *, status=None, out=None, band=None):
         op = self.options
         ds = op.ds()
         bc = {} if bc is None else bc
@@ -259,7 +277,8 @@ class Disort(RTSolver):
             keep += [tf, wl, wu]
         nlev = ds.ntau if self.radiance else nlyr + 1
         if out is None:
-            flux = torch.empty((nwave, ncol, nlev, 2), dtype=f64, device=dev)
+            flux = None if band is not None else \
+                torch.empty((nwave, ncol, nlev, 2), dtype=f64, device=dev)
         else:
             if (out.device != dev or out.dtype != f64 or not out.is_contiguous()
                     or tuple(out.shape) != (nwave, ncol, nlev, 2)):
@@ -285,6 +304,26 @@ class Disort(RTSolver):
                             fisot=ptr(bct.get("fisot")), temf=ptr(tf), wave_lower=ptr(wl),
                             wave_upper=ptr(wu))
         stream = torch.cuda.current_stream(dev)
+        if band is not None:
+            wts = torch.as_tensor(band[0], dtype=f64).to(dev).reshape(-1).contiguous()
+            if wts.numel() != nwave:
+                raise RuntimeError(f"Disort.forward_band: {wts.numel()} weights for {nwave} "
+                                   "waves")
+            bout = band[1]
+            if bout is None:
+                bout = torch.empty((ncol, nlyr + 1, 2), dtype=f64, device=dev)
+            elif (bout.device != dev or bout.dtype != f64 or not bout.is_contiguous()
+                  or tuple(bout.shape) != (ncol, nlyr + 1, 2)):
+                raise RuntimeError("Disort.forward_band: out must be a contiguous float64 "
+                                   f"tensor of shape {(ncol, nlyr + 1, 2)} on {dev}")
+            keep.append(wts)
+            hb = _lib.HdBand(weight=wts.data_ptr(), bflux=bout.data_ptr())
+            with torch.cuda.device(dev):
+                _context(dev.index).solve_band(cfg, inp, hb, ptr(flux),
+                                               status.data_ptr() if status is not None else None,
+                                               stream.cuda_stream)
+            del keep
+            return bout.to(in_dev) if in_dev.type != "cuda" else bout
         if self.radiance:
             self._forward_radiance(cfg, inp, flux, status, stream, bc, dev, keep, nwave, ncol)
         else:
