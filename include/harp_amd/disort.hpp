@@ -226,75 +226,49 @@ class DisortImpl : public torch::nn::Cloneable<DisortImpl> {
   //! forward(prop, &bc, layer2level(...)) as radiation_band.cpp:124-127 calls them.
   torch::Tensor forward(torch::Tensor prop, std::map<std::string, torch::Tensor>* bc,
                         torch::Tensor temf = torch::Tensor()) {
-    TORCH_CHECK(prop.dim() == 4, "Disort.forward: prop must be (nwave, ncol, nlyr, nprop)");
-    const int nwave = prop.size(0), ncol = prop.size(1), nlyr = prop.size(2),
-              nprop = prop.size(3);
-    TORCH_CHECK(nlyr == options.ds().nlyr, "Disort.forward: prop has ", nlyr,
-                " layers, ds().nlyr = ", options.ds().nlyr);
-    TORCH_CHECK(!planck_ || temf.defined(), "Disort.forward: planck flag set but temf missing");
-    TORCH_CHECK(!planck_ || ((int)options.wave_lower().size() == nwave &&
-                             (int)options.wave_upper().size() == nwave),
-                "Disort.forward: planck: prop has ", nwave, " waves but wave_lower/wave_upper hold ",
-                options.wave_lower().size(), "/", options.wave_upper().size());
-    auto in_dev = prop.device();
-    torch::Device dev = in_dev.is_cuda() ? in_dev : torch::Device(torch::kCUDA, options.device());
-    auto f64 = torch::TensorOptions().dtype(torch::kFloat64).device(dev);
-    auto to_dev = [&](torch::Tensor t) { return t.to(f64).contiguous(); };
-
-    auto p = to_dev(prop);
-    static const char* keys[] = {"fbeam", "umu0", "albedo", "btemp", "ttemp", "temis", "fisot"};
-    std::map<std::string, torch::Tensor> b;
-    if (bc) {
-      for (auto const& [k, v] : *bc) {
-        bool ok = k == "phi0";
-        for (auto key : keys) ok = ok || k == key;
-        TORCH_CHECK(ok, "Disort.forward: unknown boundary condition '", k, "'");
-        auto t = to_dev(v.expand({nwave, ncol}));
-        b[k] = t;
-      }
-    }
-    torch::Tensor tf, wl, wu;
-    if (planck_) {
-      tf = to_dev(temf);
-      TORCH_CHECK(tf.size(0) == ncol && tf.size(1) == nlyr + 1,
-                  "Disort.forward: temf must be (ncol, nlyr+1)");
-      wl = torch::tensor(options.wave_lower(), f64);
-      wu = torch::tensor(options.wave_upper(), f64);
-    }
-    const int nlev = radiance_ ? options.ds().ntau : nlyr + 1;
-    auto flux = torch::empty({nwave, ncol, nlev, 2}, f64);
-
-    auto ptr = [](const torch::Tensor& t) -> const double* {
-      return t.defined() ? t.data_ptr<double>() : nullptr;
-    };
-    auto bp = [&](const char* k) -> const double* {
-      auto it = b.find(k);
-      return it == b.end() ? nullptr : it->second.data_ptr<double>();
-    };
-    hd_config cfg{options.ds().nstr, options.ds().nmom, nlyr, nprop,
-                  HD_FLAG_LAMBER | HD_FLAG_ONLYFL | (planck_ ? HD_FLAG_PLANCK : 0u)};
-    hd_inputs in{nwave,       ncol,        ptr(p),        bp("fbeam"), bp("umu0"),
-                 bp("albedo"), bp("btemp"), bp("ttemp"),  bp("temis"), bp("fisot"),
-                 ptr(tf),     ptr(wl),     ptr(wu)};
-    auto stream = at::hip::getCurrentHIPStream(dev.index()).stream();
+    Batch x = prepare(prop, bc, temf);
+    const int nlev = radiance_ ? options.ds().ntau : x.nlyr + 1;
+    auto flux = torch::empty({x.nwave, x.ncol, nlev, 2}, x.f64);
+    auto stream = at::hip::getCurrentHIPStream(x.dev.index()).stream();
     int rc;
     if (radiance_) {
       auto const& d = options.ds();
       hd_radiance rad{usrtau_ ? d.ntau : 0, d.utau.data(), (int)umu_.size(), umu_.data(),
-                      (int)phi_.size(), phi_.data(), bp("phi0"), onlyfl_ ? 1 : 0,
+                      (int)phi_.size(), phi_.data(), x.bp("phi0"), onlyfl_ ? 1 : 0,
                       corint_ ? 1 : 0};
       torch::Tensor uu;
-      if (!onlyfl_) uu = torch::empty({nwave, ncol, (int)phi_.size(), d.ntau, (int)umu_.size()}, f64);
-      rc = hd_solve_radiance(context(dev.index()), &cfg, &in, &rad, flux.data_ptr<double>(),
+      if (!onlyfl_)
+        uu = torch::empty({x.nwave, x.ncol, (int)phi_.size(), d.ntau, (int)umu_.size()}, x.f64);
+      rc = hd_solve_radiance(context(x.dev.index()), &x.cfg, &x.in, &rad,
+                             flux.data_ptr<double>(),
                              uu.defined() ? uu.data_ptr<double>() : nullptr, nullptr,
                              reinterpret_cast<void*>(stream));
-      rad_ = uu.defined() ? (in_dev.is_cuda() ? uu : uu.to(in_dev)) : uu;
+      rad_ = uu.defined() ? (x.in_dev.is_cuda() ? uu : uu.to(x.in_dev)) : uu;
     } else {
-      rc = hd_solve(context(dev.index()), &cfg, &in, flux.data_ptr<double>(), nullptr,
+      rc = hd_solve(context(x.dev.index()), &x.cfg, &x.in, flux.data_ptr<double>(), nullptr,
                     reinterpret_cast<void*>(stream));
     }
-    TORCH_CHECK(rc == HD_OK, "DisortWrapper::Run failed: ", hd_last_error(context(dev.index())));
-    return in_dev.is_cuda() ? flux : flux.to(in_dev);
+    TORCH_CHECK(rc == HD_OK, "DisortWrapper::Run failed: ", hd_last_error(context(x.dev.index())));
+    return x.in_dev.is_cuda() ? flux : flux.to(x.in_dev);
+  }
+
+  //! band flux (ncol, nlyr+1, 2) = sum_w weights[w] flux[w] with the sum fused into
+  //! the solve (hd_solve_band): what examples/amars_lw.cpp:84-88 forms from
+  //! forward's result, without storing the per-point fluxes
+  torch::Tensor forward_band(torch::Tensor prop, std::map<std::string, torch::Tensor>* bc,
+                             torch::Tensor temf, torch::Tensor weights) {
+    TORCH_CHECK(!radiance_, "Disort.forward_band: the fused band sum is a flux-only path");
+    Batch x = prepare(prop, bc, temf);
+    auto w = weights.to(x.f64).reshape({-1}).contiguous();
+    TORCH_CHECK(w.size(0) == x.nwave, "Disort.forward_band: ", w.size(0), " weights for ",
+                x.nwave, " waves");
+    auto bflux = torch::empty({x.ncol, x.nlyr + 1, 2}, x.f64);
+    hd_band band{w.data_ptr<double>(), bflux.data_ptr<double>()};
+    auto stream = at::hip::getCurrentHIPStream(x.dev.index()).stream();
+    const int rc = hd_solve_band(context(x.dev.index()), &x.cfg, &x.in, &band, nullptr, nullptr,
+                                 reinterpret_cast<void*>(stream));
+    TORCH_CHECK(rc == HD_OK, "DisortWrapper::Run failed: ", hd_last_error(context(x.dev.index())));
+    return x.in_dev.is_cuda() ? bflux : bflux.to(x.in_dev);
   }
 
  protected:
@@ -305,6 +279,71 @@ class DisortImpl : public torch::nn::Cloneable<DisortImpl> {
   bool onlyfl_ = true, usrtau_ = false, radiance_ = false, corint_ = false;
   std::vector<double> umu_, phi_;
   torch::Tensor rad_;
+
+  // one batch on the device in the C-ABI's form (the tensors own the memory the
+  // hd_inputs pointers refer to)
+  struct Batch {
+    torch::Device dev = torch::kCPU, in_dev = torch::kCPU;
+    torch::TensorOptions f64;
+    int nwave = 0, ncol = 0, nlyr = 0, nprop = 0;
+    torch::Tensor p, tf, wl, wu;
+    std::map<std::string, torch::Tensor> b;
+    hd_config cfg{};
+    hd_inputs in{};
+    const double* bp(const char* k) const {
+      auto it = b.find(k);
+      return it == b.end() ? nullptr : it->second.data_ptr<double>();
+    }
+  };
+
+  Batch prepare(torch::Tensor prop, std::map<std::string, torch::Tensor>* bc,
+                torch::Tensor temf) {
+    TORCH_CHECK(prop.dim() == 4, "Disort.forward: prop must be (nwave, ncol, nlyr, nprop)");
+    Batch x;
+    x.nwave = prop.size(0);
+    x.ncol = prop.size(1);
+    x.nlyr = prop.size(2);
+    x.nprop = prop.size(3);
+    const int nwave = x.nwave, ncol = x.ncol, nlyr = x.nlyr;
+    TORCH_CHECK(nlyr == options.ds().nlyr, "Disort.forward: prop has ", nlyr,
+                " layers, ds().nlyr = ", options.ds().nlyr);
+    TORCH_CHECK(!planck_ || temf.defined(), "Disort.forward: planck flag set but temf missing");
+    TORCH_CHECK(!planck_ || ((int)options.wave_lower().size() == nwave &&
+                             (int)options.wave_upper().size() == nwave),
+                "Disort.forward: planck: prop has ", nwave, " waves but wave_lower/wave_upper hold ",
+                options.wave_lower().size(), "/", options.wave_upper().size());
+    x.in_dev = prop.device();
+    x.dev = x.in_dev.is_cuda() ? x.in_dev : torch::Device(torch::kCUDA, options.device());
+    x.f64 = torch::TensorOptions().dtype(torch::kFloat64).device(x.dev);
+    auto to_dev = [&](torch::Tensor t) { return t.to(x.f64).contiguous(); };
+    x.p = to_dev(prop);
+    static const char* keys[] = {"fbeam", "umu0", "albedo", "btemp", "ttemp", "temis", "fisot"};
+    if (bc) {
+      for (auto const& [k, v] : *bc) {
+        bool ok = k == "phi0";
+        for (auto key : keys) ok = ok || k == key;
+        TORCH_CHECK(ok, "Disort.forward: unknown boundary condition '", k, "'");
+        x.b[k] = to_dev(v.expand({nwave, ncol}));
+      }
+    }
+    if (planck_) {
+      x.tf = to_dev(temf);
+      TORCH_CHECK(x.tf.size(0) == ncol && x.tf.size(1) == nlyr + 1,
+                  "Disort.forward: temf must be (ncol, nlyr+1)");
+      x.wl = torch::tensor(options.wave_lower(), x.f64);
+      x.wu = torch::tensor(options.wave_upper(), x.f64);
+    }
+    auto ptr = [](const torch::Tensor& t) -> const double* {
+      return t.defined() ? t.data_ptr<double>() : nullptr;
+    };
+    x.cfg = hd_config{options.ds().nstr, options.ds().nmom, nlyr, x.nprop,
+                      HD_FLAG_LAMBER | HD_FLAG_ONLYFL | (planck_ ? HD_FLAG_PLANCK : 0u)};
+    x.in = hd_inputs{nwave,          ncol,          ptr(x.p),       x.bp("fbeam"),
+                     x.bp("umu0"),   x.bp("albedo"), x.bp("btemp"), x.bp("ttemp"),
+                     x.bp("temis"),  x.bp("fisot"),  ptr(x.tf),     ptr(x.wl),
+                     ptr(x.wu)};
+    return x;
+  }
 
   // one hd_context per (device, host thread) (SURVEY 8(b) "Threading"); the
   // modules of a thread share it and libhdisort orders their solves, on any

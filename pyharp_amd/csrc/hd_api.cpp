@@ -159,7 +159,8 @@ long auto_chunk(long nsolve, int nn, int nlyr, bool planck) {
   if (nn <= hd::kMaxRegNN) {
     target = 65536;
   } else {
-    const double budget = 8.0 * 1024.0 * 1024.0 * 1024.0;  // bytes of scratch per chunk
+    // bytes of scratch for the two chunks in flight (the per-solve size counts both)
+    const double budget = 16.0 * 1024.0 * 1024.0 * 1024.0;
     const double per = 8.0 * (double)hd::scratch_doubles_per_solve(nn, nlyr, planck);
     target = std::min<long>(262144, std::max<long>(16384, (long)(budget / per)));
   }
@@ -453,8 +454,11 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
   // the caller's stream (prologue, layer kernel, sweep, tail back-substitution),
   // without the fork/join of the three-stream pipeline below (C1/C3 latency)
   const bool single = reg && nsolve <= chunk;
+  // team path with several chunks: chunk k+1's prologue and layer kernel on the
+  // `lay` stream beside chunk k's sweep on the caller's stream
+  const bool team_pipe = !reg && nsolve > chunk;
   const bool beam = in->fbeam != nullptr;
-  const int nb = reg ? 2 : 1;  // buffers of the per-chunk regions that live across chunks
+  const int nb = 2;  // buffers of the per-chunk regions (two chunks in flight)
   // Scratch regions, sized for the largest chunk so that no region moves between
   // chunks (inside a region the kernels interleave with the chunk's own nsc):
   //   layer ops[nb] | bsub[nb] | xsurf[nb] | planck[nb] | tauc[nb]
@@ -533,7 +537,7 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
     pa.nwave = in->nwave;
   };
 
-  if (reg && !single) {
+  if ((reg && !single) || team_pipe) {
     // fork: the side stream sees everything the caller's stream did before this
     // call (the inputs) -- and, under stream capture, joins the graph here
     HD_HIP(ctx, hipEventRecord(ctx->ev_fork, stream));
@@ -543,11 +547,15 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
   long k = 0;  // chunk index
   for (long s0 = 0; s0 < nsolve; s0 += chunk, ++k) {
     const int nsc = (int)std::min(chunk, nsolve - s0);
-    const int buf = reg ? (int)(k & 1) : 0;
+    const int buf = (int)(k & 1);
     hd::TaucArgs ta;
     hd::PlanckArgs pa;
     prologue_args(s0, nsc, buf, ta, pa);
-    if (!reg || single) {
+    if (team_pipe) {
+      // buffer `buf` is free once sweep k-2 (its last reader) is done
+      if (k >= 2) HD_HIP(ctx, hipStreamWaitEvent(ctx->lay, ctx->ev_sweep[buf], 0));
+      hd::launch_prologue(planck ? &pa : nullptr, beam ? &ta : nullptr, ctx->lay);
+    } else if (!reg || single) {
       hd::launch_prologue(planck ? &pa : nullptr, beam ? &ta : nullptr, stream);
     } else if (k == 0) {
       hd::launch_prologue(planck ? &pa : nullptr, beam ? &ta : nullptr, ctx->side);
@@ -645,6 +653,19 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
         e = hd::launch_sweep_nn(nn, sa, stream);
         if (ev) HD_HIP(ctx, hipEventRecord(ev[3], stream));
       }
+    } else if (team_pipe) {
+      if (ev) HD_HIP(ctx, hipEventRecord(ev[0], ctx->lay));
+      e = hd::launch_team_layer_nn(nn, la, ctx->lay);
+      if (ev) HD_HIP(ctx, hipEventRecord(ev[1], ctx->lay));
+      HD_HIP(ctx, hipEventRecord(ctx->ev_layer[buf], ctx->lay));
+      if (e == hipSuccess) {
+        HD_HIP(ctx, hipStreamWaitEvent(stream, ctx->ev_layer[buf], 0));
+        if (ev) HD_HIP(ctx, hipEventRecord(ev[2], stream));
+        e = hd::launch_team_sweep_nn(nn, sa, stream);
+        if (ev) HD_HIP(ctx, hipEventRecord(ev[3], stream));
+      }
+      if (e == hipSuccess && band) e = hd::launch_band_reduce(band_args(s0, nsc), stream);
+      HD_HIP(ctx, hipEventRecord(ctx->ev_sweep[buf], stream));
     } else {
       e = hd::launch_solve_chunk_team(nn, nullptr, nullptr, la, sa, stream, ev);
       if (e == hipSuccess && band) e = hd::launch_band_reduce(band_args(s0, nsc), stream);

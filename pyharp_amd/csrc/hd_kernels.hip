@@ -1102,11 +1102,11 @@ size_t bsub_record_doubles(int nn) {
 }
 
 size_t scratch_doubles_per_solve(int nn, int nlyr, bool planck) {
-  // register path: back-substitution records, xsurf and the tauc/planck
-  // prologue are double-buffered (chunk k's back-substitution and chunk k+1's
-  // prologue run on a side stream beside the main chain), see hd_solve
-  // and the layer records too (chunk k+1's layer kernel runs beside chunk k's sweep)
-  const size_t nb = nn <= kMaxRegNN ? 2 : 1;
+  // every per-chunk region is double-buffered: chunk k+1's layer kernel (and its
+  // tauc/planck prologue) runs beside chunk k's sweep on another stream, and on
+  // the register path chunk k's back-substitution beside chunk k+1's layer
+  // kernel on a third (see hd_solve)
+  const size_t nb = 2;
   return nb * (layer_record_doubles(nn) * nlyr + bsub_record_doubles(nn) * nlyr + 1 +
                (planck ? (size_t)nlyr + 3 : 0) + (size_t)nlyr);
 }

@@ -159,6 +159,9 @@ hipError_t launch_sweep_nn(int nn, const SweepArgs& sa, hipStream_t stream);
 hipError_t launch_solve_chunk_team(int nn, const PlanckArgs* pa, const TaucArgs* ta,
                                    const LayerArgs& la, const SweepArgs& sa, hipStream_t stream,
                                    hipEvent_t* ev);
+// team path, separately: the layer kernel and the sweep of one chunk
+hipError_t launch_team_layer_nn(int nn, const LayerArgs& la, hipStream_t stream);
+hipError_t launch_team_sweep_nn(int nn, const SweepArgs& sa, hipStream_t stream);
 size_t scratch_doubles_per_solve(int nn, int nlyr, bool planck);
 // the chunk epilogue of hd_solve_band (after the chunk's back-substitution)
 hipError_t launch_band_reduce(const BandArgs& ba, hipStream_t stream);

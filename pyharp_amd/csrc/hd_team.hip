@@ -606,6 +606,53 @@ static hipError_t launch_team(const PlanckArgs* pa, const TaucArgs* ta, const La
   return hipGetLastError();
 }
 
+// the two halves of launch_team, for the pipelined multi-chunk path of hd_solve
+// (chunk k+1's layer kernel on one stream beside chunk k's sweep on another)
+template <int NN>
+static hipError_t launch_team_layer(const LayerArgs& la, hipStream_t stream) {
+  if (team_layer_valu()) {
+    const long nt1 = (long)la.nsc * la.nlyr;
+    const unsigned nb1 = (unsigned)((nt1 + kTeamsPerBlock - 1) / kTeamsPerBlock);
+    hipLaunchKernelGGL(hd_team_layer_kernel<NN>, dim3(nb1), dim3(kTeamBlock), 0, stream, la);
+    return hipGetLastError();
+  }
+  return launch_team_layer_mfma(NN, la, stream);
+}
+template <int NN>
+static hipError_t launch_team_sweep(const SweepArgs& sa, hipStream_t stream) {
+  const unsigned nb2 = (unsigned)((sa.nsc + kTeamsPerBlock - 1) / kTeamsPerBlock);
+  hipLaunchKernelGGL(hd_team_sweep_kernel<NN>, dim3(nb2), dim3(kTeamBlock), 0, stream, sa);
+  return hipGetLastError();
+}
+
+hipError_t launch_team_layer_nn(int nn, const LayerArgs& la, hipStream_t stream) {
+  switch (nn) {
+    case 9: return launch_team_layer<9>(la, stream);
+    case 10: return launch_team_layer<10>(la, stream);
+    case 11: return launch_team_layer<11>(la, stream);
+    case 12: return launch_team_layer<12>(la, stream);
+    case 13: return launch_team_layer<13>(la, stream);
+    case 14: return launch_team_layer<14>(la, stream);
+    case 15: return launch_team_layer<15>(la, stream);
+    case 16: return launch_team_layer<16>(la, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_team_sweep_nn(int nn, const SweepArgs& sa, hipStream_t stream) {
+  switch (nn) {
+    case 9: return launch_team_sweep<9>(sa, stream);
+    case 10: return launch_team_sweep<10>(sa, stream);
+    case 11: return launch_team_sweep<11>(sa, stream);
+    case 12: return launch_team_sweep<12>(sa, stream);
+    case 13: return launch_team_sweep<13>(sa, stream);
+    case 14: return launch_team_sweep<14>(sa, stream);
+    case 15: return launch_team_sweep<15>(sa, stream);
+    case 16: return launch_team_sweep<16>(sa, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 hipError_t launch_solve_chunk_team(int nn, const PlanckArgs* pa, const TaucArgs* ta,
                                    const LayerArgs& la, const SweepArgs& sa, hipStream_t stream,
                                    hipEvent_t* ev) {

@@ -35,5 +35,12 @@ int main(int argc, char** argv) {
     for (int c = 0; c < ncol; ++c)
       for (int l = 0; l <= nlyr; ++l)
         std::printf("%d %d %d %.17g %.17g\n", w, c, l, acc[w][c][l][0], acc[w][c][l][1]);
+  // the band sum amars_lw.cpp:84-88 forms next, fused into the solve
+  auto wts = 1.0 + 0.1 * torch::arange(nwave, torch::kFloat64);
+  auto band = disort->forward_band(prop, &bc, torch::Tensor(), wts).cpu();
+  auto bacc = band.accessor<double, 3>();
+  for (int c = 0; c < ncol; ++c)
+    for (int l = 0; l <= nlyr; ++l)
+      std::printf("band %d %d %.17g %.17g\n", c, l, bacc[c][l][0], bacc[c][l][1]);
   return 0;
 }

@@ -152,17 +152,20 @@ def test_aerosol_config_subsample(oracle_c):
     assert err < TOL, f"max rel err {err:.3e}"
 
 
-@pytest.mark.parametrize("nstr", [8, 24])
-def test_chunking_invariance_team(nstr):
-    rng = np.random.default_rng(70 + nstr)
-    prop, bc, _ = _random_batch(rng, 3, 37, 12, nstr, False)
-    d = _disort(nstr, 12, 3, 37)
-    f1 = _run(d, prop, bc)
+@pytest.mark.parametrize("nstr,planck", [(8, False), (24, False), (24, True), (32, True)])
+def test_chunking_invariance_team(nstr, planck):
+    """Several chunks: the two-stream pipelines (team path: chunk k+1's prologue and
+    layer kernel beside chunk k's sweep) give the single-chunk fluxes bit for bit."""
+    rng = np.random.default_rng(70 + nstr + planck)
+    prop, bc, kw = _random_batch(rng, 3, 37, 12, nstr, planck)
+    d = _disort(nstr, 12, 3, 37, planck=planck, wl=kw.get("wave_lower"),
+                wu=kw.get("wave_upper"))
+    f1 = _run(d, prop, bc, kw.get("temf"))
     from pyharp_amd.disort import _context
     ctx = _context(0)
     ctx.set_chunk(17)
     try:
-        f2 = _run(d, prop, bc)
+        f2 = _run(d, prop, bc, kw.get("temf"))
     finally:
         ctx.set_chunk(0)
     assert np.array_equal(f1, f2)
@@ -282,7 +285,12 @@ def test_cpp_dropin(oracle_c):
     out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout
     nwave, ncol, nlyr, nstr = 6, 2, 12, 8
     got = np.zeros((nwave, ncol, nlyr + 1, 2))
+    band = np.zeros((ncol, nlyr + 1, 2))
     for line in out.strip().splitlines():
+        if line.startswith("band "):  # Disort::forward_band (hd_solve_band)
+            _, c, l, up, dn = line.split()
+            band[int(c), int(l)] = (float(up), float(dn))
+            continue
         w, c, l, up, dn = line.split()
         got[int(w), int(c), int(l)] = (float(up), float(dn))
     prop = np.zeros((nwave, ncol, nlyr, 2))
@@ -295,6 +303,8 @@ def test_cpp_dropin(oracle_c):
           "albedo": np.ones((nwave, ncol))}
     ref = oracle_c.forward(prop, bc, nstr=nstr)
     assert rel_err(got, ref).max() < TOL
+    bref = np.einsum("w,wclk->clk", 1.0 + 0.1 * np.arange(nwave), ref)
+    assert rel_err(band, bref).max() < TOL
 
 
 def _lw_problem(G, nstr, nlyr, tau, band, ck, seed=20250217):
