@@ -1,11 +1,18 @@
-// harp_amd/ncread.hpp -- header-only reader of netCDF *classic* files (CDF-1,
-// CDF-2 64-bit offset, CDF-5) for the RFM opacity tables and ck weights that
-// harp reads with nc_inq_dimid / nc_inq_dimlen / nc_inq_varid /
-// nc_get_var_double (src/opacity/rfm.cpp:30-120, src/utils/read_weights.cpp:18-46).
-// The netCDF library is not a dependency; netCDF-4 (HDF5) files are refused
-// with a message (convert once with `nccopy -k classic`).  Mirrors
-// pyharp_amd/ncread.py.
+// harp_amd/ncread.hpp -- header-only readers of the netCDF files harp opens for
+// the RFM opacity tables and ck weights with nc_open / nc_inq_dimid /
+// nc_inq_dimlen / nc_inq_varid / nc_get_var_double (src/opacity/rfm.cpp:34-120,
+// src/utils/read_weights.cpp:18-46):
+//   NetCDFClassic  classic files (CDF-1, CDF-2 64-bit offset, CDF-5)
+//   NetCDF4        netCDF-4 / HDF5 files, the format rfm.cpp:39 opens
+//                  (nc_open(..., NC_NETCDF4, ...)) -- harp_amd/nc4read.hpp
+//   NetCDFFile     either, chosen by the file's signature (what nc_open does)
+// The netCDF library is not a dependency (NetCDF4 needs zlib: link -lz).
+// Mirrors pyharp_amd/ncread.py.
 #pragma once
+
+#include "nc4read.hpp"
+
+#include <memory>
 
 #include <cstdint>
 #include <cstring>
@@ -34,8 +41,8 @@ class NetCDFClassic {
     buf_.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
     if (buf_.size() >= 4 && (unsigned char)buf_[0] == 0x89 && buf_[1] == 'H' && buf_[2] == 'D' &&
         buf_[3] == 'F')
-      throw std::runtime_error(path + ": netCDF-4/HDF5 file; this reader takes classic netCDF "
-                                      "only (convert with `nccopy -k classic`)");
+      throw std::runtime_error(path + ": netCDF-4/HDF5 file; NetCDFClassic takes classic netCDF "
+                                      "only (NetCDFFile / NetCDF4 read it)");
     if (buf_.size() < 8 || buf_[0] != 'C' || buf_[1] != 'D' || buf_[2] != 'F' ||
         (buf_[3] != 1 && buf_[3] != 2 && buf_[3] != 5))
       throw std::runtime_error(path + ": not a netCDF classic file");
@@ -173,6 +180,28 @@ class NetCDFClassic {
       default: throw std::runtime_error("ncread: char variables are not numeric");
     }
   }
+};
+
+//! nc_open: a classic or a netCDF-4 (HDF5) file, by signature
+class NetCDFFile {
+ public:
+  explicit NetCDFFile(std::string const& path) {
+    if (NetCDF4::is_hdf5(path))
+      h5_ = std::make_unique<NetCDF4>(path);
+    else
+      cl_ = std::make_unique<NetCDFClassic>(path);
+  }
+  bool netcdf4() const { return h5_ != nullptr; }
+  size_t dim_len(std::string const& name) const {
+    return h5_ ? h5_->dim_len(name) : cl_->dim_len(name);
+  }
+  std::vector<double> var(std::string const& name) const {
+    return h5_ ? h5_->var(name) : cl_->var(name);
+  }
+
+ private:
+  std::unique_ptr<NetCDF4> h5_;
+  std::unique_ptr<NetCDFClassic> cl_;
 };
 
 }  // namespace harp_amd

@@ -1,7 +1,7 @@
 // harp_amd/opacity.hpp -- libtorch drop-ins for pyharp's table attenuators
 // (harp::S8Fuller, harp::H2SO4Simple; src/opacity/s8_fuller.cpp,
 // src/opacity/h2so4_simple.cpp), the RFM absorption tables (harp::RFM,
-// src/opacity/rfm.cpp; tables read from classic netCDF by ncread.hpp),
+// src/opacity/rfm.cpp; tables read from netCDF-4 or classic files by ncread.hpp),
 // read_weights_rfm (src/utils/read_weights.cpp) and the SW example's optics
 // assembly (examples/amars_sw.cpp:261-271), backed by libhdisort.so (include/hdharp.h).
 //
@@ -263,7 +263,7 @@ class RFMImpl : public torch::nn::Cloneable<RFMImpl> {
   }
 
   void reset() override {
-    NetCDFClassic nc(find_resource(options.opacity_files()[0]));
+    NetCDFFile nc(find_resource(options.opacity_files()[0]));
     kshape[0] = nc.dim_len("Wavenumber");
     kshape[1] = nc.dim_len("Pressure");
     kshape[2] = nc.dim_len("TempGrid");
@@ -321,7 +321,7 @@ TORCH_MODULE(RFM);
 
 //! src/utils/read_weights.cpp:18-46
 inline torch::Tensor read_weights_rfm(std::string const& filename) {
-  NetCDFClassic nc(find_resource(filename));
+  NetCDFFile nc(find_resource(filename));
   const size_t n = nc.dim_len("weights");
   auto w = nc.var("weights");
   TORCH_CHECK(w.size() == n, "read_weights_rfm: size mismatch");

@@ -14,9 +14,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libhdisort.so")
 SOURCES = ["hd_kernels.hip", "hd_team.hip", "hd_team_mfma.hip", "hd_rad.hip", "hd_harp.hip",
-           "hd_api.cpp"]
+           "hd_api.cpp", "hd_ncread.cpp"]
 HEADERS = ["hd_device.hpp", "hd_kernels.hpp", "hd_rad.hpp", "hd_team_prims.hpp", os.path.join("..", "..", "include", "hdisort.h"),
-           os.path.join("..", "..", "include", "hdharp.h")]
+           os.path.join("..", "..", "include", "hdharp.h"),
+           os.path.join("..", "..", "include", "hdnc.h"),
+           os.path.join("..", "..", "include", "harp_amd", "ncread.hpp"),
+           os.path.join("..", "..", "include", "harp_amd", "nc4read.hpp")]
 ARCH = os.environ.get("HD_OFFLOAD_ARCH", "gfx950")
 
 
@@ -53,7 +56,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if p.wait() != 0:
             raise subprocess.CalledProcessError(p.returncode, cmd)
     tmp = LIB + ".tmp"
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + ["-lz"]
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
     for o in objs:

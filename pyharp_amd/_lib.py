@@ -33,6 +33,10 @@ HARP_EXPORTED = ("hd_attenuate", "hd_band_optics", "hd_rfm_attenuate", "hd_band_
                  "hd_heating_rate", "hd_spherical_flux_correction")
 HD_COORD_WAVELENGTH, HD_COORD_WAVENUMBER = 0, 1
 
+# every symbol include/hdnc.h declares (netCDF readers, host code)
+NC_EXPORTED = ("hd_nc_open", "hd_nc_close", "hd_nc_dim_len", "hd_nc_var_size",
+               "hd_nc_get_var_double")
+
 _dp = ctypes.c_void_p
 
 
@@ -120,7 +124,14 @@ def load(path: str = LIB_PATH):
     lib.hd_band_flux.argtypes = [_dp, _dp, ci, ci, ci, _dp, _dp]
     lib.hd_heating_rate.argtypes = [_dp, _dp, _dp, cd, ci, ci, _dp, _dp]
     lib.hd_spherical_flux_correction.argtypes = [_dp, _dp, _dp, _dp, ci, ci, _dp]
-    for name in EXPORTED + HARP_EXPORTED:
+    lib.hd_nc_open.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p),
+                               ctypes.POINTER(ctypes.c_int)]
+    lib.hd_nc_close.argtypes = [ctypes.c_void_p]
+    lib.hd_nc_dim_len.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_long)]
+    lib.hd_nc_var_size.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_long)]
+    lib.hd_nc_get_var_double.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p,
+                                         ctypes.c_long]
+    for name in EXPORTED + HARP_EXPORTED + NC_EXPORTED:
         getattr(lib, name)
     _lib = lib
     return lib

@@ -1,13 +1,15 @@
-"""Minimal reader of netCDF *classic* files (CDF-1, CDF-2 64-bit offset, CDF-5)
-for the opacity tables the RFM attenuator and ``read_weights_rfm`` load
-(``src/opacity/rfm.cpp:30-120``, ``src/utils/read_weights.cpp:18-46``: the
-``nc_inq_dimid / nc_inq_dimlen / nc_inq_varid / nc_get_var_double`` calls).
+"""Readers of the netCDF files the RFM attenuator and ``read_weights_rfm`` load
+(``src/opacity/rfm.cpp:34-120``, ``src/utils/read_weights.cpp:18-46``: the
+``nc_open / nc_inq_dimid / nc_inq_dimlen / nc_inq_varid / nc_get_var_double``
+calls).  The netCDF library is not in this image; this is host-side file parsing:
 
-The netCDF library is not in this image; this is host-side file parsing only
-(big-endian header + contiguous variables, as laid out by the classic format
-specification).  netCDF-4 files (HDF5 containers) are recognised and refused
-with a clear message: converting them once with ``nccopy -k classic`` gives a
-file this reader takes.
+* ``NetCDFClassic`` -- classic files (CDF-1, CDF-2 64-bit offset, CDF-5), pure
+  Python (big-endian header + contiguous variables, per the classic format
+  specification);
+* ``NetCDF4`` -- netCDF-4 files (HDF5 containers, what rfm.cpp:39 opens with
+  ``NC_NETCDF4``), through the C-ABI of ``include/hdnc.h`` over the HDF5-format
+  walker of ``include/harp_amd/nc4read.hpp`` (in libhdisort.so);
+* ``open_netcdf`` -- either, by the file's signature (as ``nc_open`` does).
 """
 
 from __future__ import annotations
@@ -31,8 +33,8 @@ class NetCDFClassic:
         with open(path, "rb") as f:
             head = f.read(8)
             if head[:4] == b"\x89HDF":
-                raise RuntimeError(f"{path}: netCDF-4/HDF5 file; this reader takes classic "
-                                   "netCDF only (convert with `nccopy -k classic`)")
+                raise RuntimeError(f"{path}: netCDF-4/HDF5 file; NetCDFClassic takes classic "
+                                   "netCDF only (open_netcdf / NetCDF4 read it)")
             if head[:3] != b"CDF" or head[3] not in (1, 2, 5):
                 raise RuntimeError(f"{path}: not a netCDF classic file")
             self.version = head[3]
@@ -128,3 +130,65 @@ class NetCDFClassic:
                               offset=v["begin"] + r * self.recsize)
                 for r in range(self.numrecs)]
         return np.stack(rows).astype(np.float64).reshape([self.numrecs] + v["shape"][1:])
+
+
+class NetCDF4:
+    """A netCDF-4 (HDF5) file read through libhdisort.so's hdnc.h: ``dim_len`` is the
+    extent of the dataset of that name (the coordinate variable or netCDF's
+    dimension scale), ``var`` the whole variable as float64 in C order."""
+
+    def __init__(self, path: str):
+        import ctypes
+        from . import _lib
+        self.path = path
+        self._lib = _lib.load()
+        h = ctypes.c_void_p()
+        is4 = ctypes.c_int(0)
+        _lib.check(self._lib.hd_nc_open(path.encode(), ctypes.byref(h), ctypes.byref(is4)))
+        self._h = h
+        if not is4.value:
+            self.close()
+            raise RuntimeError(f"{path}: not a netCDF-4/HDF5 file (use NetCDFClassic)")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.hd_nc_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, name):
+        from . import _lib
+        if rc != _lib.HD_OK:
+            msg = _lib.last_error()
+            raise RuntimeError(msg or f"{self.path}: {name}")
+
+    def dim_len(self, name: str) -> int:
+        import ctypes
+        n = ctypes.c_long(0)
+        self._check(self._lib.hd_nc_dim_len(self._h, name.encode(), ctypes.byref(n)), name)
+        return int(n.value)
+
+    def var(self, name: str) -> np.ndarray:
+        """nc_get_var_double: the whole variable as float64, C order (flat when the
+        file's shape is not needed; see ``shape``)."""
+        import ctypes
+        n = ctypes.c_long(0)
+        self._check(self._lib.hd_nc_var_size(self._h, name.encode(), ctypes.byref(n)), name)
+        out = np.empty(int(n.value), dtype=np.float64)
+        self._check(self._lib.hd_nc_get_var_double(
+            self._h, name.encode(), out.ctypes.data_as(ctypes.c_void_p), n), name)
+        return out
+
+
+def open_netcdf(path: str):
+    """nc_open: NetCDF4 for an HDF5 container, else NetCDFClassic."""
+    with open(path, "rb") as f:
+        head = f.read(8)
+    if head == b"\x89HDF\r\n\x1a\n":
+        return NetCDF4(path)
+    return NetCDFClassic(path)

@@ -240,7 +240,7 @@ class RFM:
     (pressure converted to ln p), the reference ``Temperature`` profile, and
     the absorption variable named after ``species_names[species_ids[0]]``
     (nwave, npres, ntemp) in ln(m^2/kmol) -- through the classic-netCDF reader
-    (``pyharp_amd.ncread``; netCDF-4/HDF5 files are refused).  ``from_arrays``
+    (``pyharp_amd.ncread``: netCDF-4/HDF5 as rfm.cpp:39 opens them, or classic).  ``from_arrays``
     builds the same module from in-memory tables.  ``forward(conc, kwargs)``
     with ``kwargs["pres"]`` [Pa] and ``kwargs["temp"]`` [K] (ncol, nlyr) returns
     (nwave, ncol, nlyr, 1) = 1e-3 exp(k) conc [1/m], interpolated on the device
@@ -286,9 +286,9 @@ class RFM:
         self._dev_tables = {}
 
     def reset(self):
-        from .ncread import NetCDFClassic
+        from .ncread import open_netcdf
         path = find_resource(self.options.opacity_files()[0])
-        nc = NetCDFClassic(path)
+        nc = open_netcdf(path)  # rfm.cpp:39 nc_open(..., NC_NETCDF4, ...); classic too
         nw, npr, nt = (nc.dim_len("Wavenumber"), nc.dim_len("Pressure"),
                        nc.dim_len("TempGrid"))
         name = self.options.species_names()[self.options.species_ids()[0]]
@@ -338,7 +338,7 @@ class RFM:
 
 def read_weights_rfm(filename: str) -> torch.Tensor:
     """src/utils/read_weights.cpp:18-46: the ``weights`` variable of an RFM ck file."""
-    from .ncread import NetCDFClassic
-    nc = NetCDFClassic(find_resource(filename))
+    from .ncread import open_netcdf
+    nc = open_netcdf(find_resource(filename))
     n = nc.dim_len("weights")
     return torch.as_tensor(nc.var("weights").reshape(n).copy())

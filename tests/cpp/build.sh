@@ -12,7 +12,7 @@ build() {
     -I"$ROOT/include" -I"$TORCH/include" -I"$TORCH/include/torch/csrc/api/include" \
     "$HERE/$1.cpp" -o "$HERE/$1" \
     -L"$TORCH/lib" -Wl,-rpath,"$TORCH/lib" -ltorch -ltorch_cpu -lc10 -ltorch_hip -lc10_hip \
-    -L"$ROOT/pyharp_amd" -Wl,-rpath,'$ORIGIN/../../pyharp_amd' -lhdisort
+    -L"$ROOT/pyharp_amd" -Wl,-rpath,'$ORIGIN/../../pyharp_amd' -lhdisort -lz
 }
 build disort_dropin &
 build amars_sw_dropin &

@@ -47,6 +47,14 @@ def test_exports_every_harp_symbol(lib):
         assert hasattr(lib, name), name
 
 
+def test_exports_every_netcdf_symbol(lib):
+    from pyharp_amd import _lib
+    names = _declared_functions("hdnc.h")
+    assert set(names) == set(_lib.NC_EXPORTED)
+    for name in names:
+        assert hasattr(lib, name), name
+
+
 def test_harp_ops_refuse_cpu_tensors():
     from pyharp_amd.spectral import band_flux, heating_rate
     with pytest.raises(RuntimeError, match="device"):

@@ -94,7 +94,7 @@ def test_cpp_reader_matches(tmp_path):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     exe = str(tmp_path / "ncread_check")
     subprocess.run(["g++", "-O1", "-std=c++17", "-I", os.path.join(root, "include"),
-                    os.path.join(root, "tests", "cpp", "ncread_check.cpp"), "-o", exe],
+                    os.path.join(root, "tests", "cpp", "ncread_check.cpp"), "-o", exe, "-lz"],
                    check=True)
     fx = write_rfm_table(str(tmp_path / "ck.nc"), version=1)
     out = subprocess.run([exe, str(tmp_path / "ck.nc"), "dim:Pressure", "Pressure", "H2O",
@@ -114,5 +114,5 @@ def test_cpp_reader_matches(tmp_path):
     np.testing.assert_array_equal(vals["weights"], fx["weights"])
     bad = tmp_path / "h.nc"
     bad.write_bytes(b"\x89HDF\r\n\x1a\n" + b"\0" * 32)
-    r = subprocess.run([exe, str(bad), "x"], capture_output=True, text=True)
+    r = subprocess.run([exe, "--classic", str(bad), "x"], capture_output=True, text=True)
     assert r.returncode == 2 and "HDF5" in r.stdout
