@@ -179,7 +179,6 @@ class DisortImpl : public torch::nn::Cloneable<DisortImpl> {
     rad_ = torch::Tensor();
     auto& d = options.ds();
     if (radiance_) {
-      TORCH_CHECK(d.nstr <= 16, "Disort: radiances / user depths need nstr <= 16");
       if (usrtau_) {
         d.utau = options.user_tau();
         TORCH_CHECK(!d.utau.empty(), "Disort: usrtau set but user_tau is empty");

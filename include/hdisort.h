@@ -156,7 +156,8 @@ int hd_solve_band(hd_context *ctx, const hd_config *cfg, const hd_inputs *in,
  * tests/test_disort.cpp:13-55 (user_mu, user_phi, user_tau; get_rad at :52)
  * and by the legacy driver src/rtsolver/rt_solver_disort.cpp_:210-286
  * (c_disort, then ds_out_.uu interpolated onto outgoing rays).  Every
- * azimuthal mode m < nstr (mode 0 only without a beam), nstr <= 16.
+ * azimuthal mode m < nstr (mode 0 only without a beam), every nstr 2..32
+ * (nstr 18..32: the same kernels with their per-lane matrices in private memory).
  *
  *   utau   HOST [ntau] user optical depths (unscaled, >= 0, ascending);
  *          ntau = 0: the nlyr+1 layer boundaries of every column

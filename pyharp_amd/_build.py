@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libhdisort.so")
 SOURCES = ["hd_kernels.hip", "hd_team.hip", "hd_team_mfma.hip", "hd_rad.hip", "hd_harp.hip",
-           "hd_api.cpp", "hd_ncread.cpp"]
+           "hd_api.cpp", "hd_ncread.cpp", "hd_rad_wide.hip"]
 HEADERS = ["hd_device.hpp", "hd_kernels.hpp", "hd_rad.hpp", "hd_team_prims.hpp", os.path.join("..", "..", "include", "hdisort.h"),
            os.path.join("..", "..", "include", "hdharp.h"),
            os.path.join("..", "..", "include", "hdnc.h"),

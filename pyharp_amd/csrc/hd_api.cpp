@@ -862,7 +862,9 @@ int rad_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in,
 
   const size_t nuc = (size_t)nm_mode * chunk;  // units of the largest chunk
   double* q = ctx->scratch;
-  double* r_sw = q;   q += (size_t)nlyr * hd::layer_record_doubles(nn) * nuc;
+  // the intensity kernels keep the register-path layer record layout at every
+  // nstr (hd::layer_record_doubles gives the team layout above nstr 16)
+  double* r_sw = q;   q += (size_t)nlyr * hd::rad_layer_record_doubles(nn) * nuc;
   double* r_rd = q;   q += (size_t)nlyr * hd::rad_rec_doubles(nn) * nuc;
   double* r_bs = q;   q += (size_t)nlyr * hd::rad_bsub_doubles(nn) * nuc;
   double* r_lev = q;  q += (size_t)(nlyr + 1) * 2 * nn * nuc;

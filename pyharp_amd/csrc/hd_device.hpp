@@ -145,23 +145,30 @@ __device__ inline double plkavg(double wlo, double whi, double t) {
 // In-place Cholesky: reads the SPD matrix from the upper triangle of a and
 // writes the lower factor (diagonal included) into the lower triangle of the
 // same array (the strict upper triangle keeps the input); rd = 1/diag(L).
+// NN-loops of the per-lane matrix helpers: fully unrolled (matrices in
+// registers) -- unless the including translation unit asks for rolled loops
+// (hd_rad_wide.hip: the intensity path at nstr 18..32, matrices in private memory)
+#ifndef HD_UNROLL_NN
+#define HD_UNROLL_NN _Pragma("unroll")
+#endif
+
 template <int NN>
 __device__ __forceinline__ bool chol_inplace(double (&a)[NN][NN], double (&rd)[NN]) {
   bool ok = true;
-#pragma unroll
+HD_UNROLL_NN
   for (int j = 0; j < NN; ++j) {
     double s = a[j][j];
-#pragma unroll
+HD_UNROLL_NN
     for (int k = 0; k < j; ++k) s = fma(-a[j][k], a[j][k], s);
     ok = ok && (s > 0.0);
     s = s > 1e-300 ? s : 1e-300;
     const double r = rsq_nr(s);
     a[j][j] = s * r;
     rd[j] = r;
-#pragma unroll
+HD_UNROLL_NN
     for (int i = j + 1; i < NN; ++i) {
       double t = a[j][i];
-#pragma unroll
+HD_UNROLL_NN
       for (int k = 0; k < j; ++k) t = fma(-a[i][k], a[j][k], t);
       a[i][j] = t * r;
     }
@@ -173,10 +180,10 @@ __device__ __forceinline__ bool chol_inplace(double (&a)[NN][NN], double (&rd)[N
 template <int NN>
 __device__ __forceinline__ void lower_solve(const double (&l)[NN][NN], const double (&rd)[NN],
                                             double (&x)[NN]) {
-#pragma unroll
+HD_UNROLL_NN
   for (int i = 0; i < NN; ++i) {
     double s = x[i];
-#pragma unroll
+HD_UNROLL_NN
     for (int k = 0; k < i; ++k) s = fma(-l[i][k], x[k], s);
     x[i] = s * rd[i];
   }
@@ -186,10 +193,10 @@ __device__ __forceinline__ void lower_solve(const double (&l)[NN][NN], const dou
 template <int NN>
 __device__ __forceinline__ void lower_t_solve(const double (&l)[NN][NN], const double (&rd)[NN],
                                               double (&x)[NN]) {
-#pragma unroll
+HD_UNROLL_NN
   for (int i = NN - 1; i >= 0; --i) {
     double s = x[i];
-#pragma unroll
+HD_UNROLL_NN
     for (int k = i + 1; k < NN; ++k) s = fma(-l[k][i], x[k], s);
     x[i] = s * rd[i];
   }
@@ -201,23 +208,23 @@ __device__ __forceinline__ void lower_t_solve(const double (&l)[NN][NN], const d
 template <int NN>
 __device__ __forceinline__ void spd_inverse_upper(double (&a)[NN][NN], const double (&rd)[NN]) {
   double k[NN][NN];  // lower
-#pragma unroll
+HD_UNROLL_NN
   for (int j = 0; j < NN; ++j) {
     k[j][j] = rd[j];
-#pragma unroll
+HD_UNROLL_NN
     for (int i = j + 1; i < NN; ++i) {
       double t = 0.0;
-#pragma unroll
+HD_UNROLL_NN
       for (int m = j; m < i; ++m) t = fma(a[i][m], k[m][j], t);
       k[i][j] = -t * rd[i];
     }
   }
-#pragma unroll
+HD_UNROLL_NN
   for (int i = 0; i < NN; ++i)
-#pragma unroll
+HD_UNROLL_NN
     for (int j = i; j < NN; ++j) {
       double t = 0.0;
-#pragma unroll
+HD_UNROLL_NN
       for (int m = j; m < NN; ++m) t = fma(k[m][i], k[m][j], t);
       a[i][j] = t;
     }
@@ -242,7 +249,7 @@ __device__ __forceinline__ void jacobi_round(int r, double (&a)[NN][NN], double 
   constexpr int P = NN + (NN & 1);
   constexpr int H = P / 2;
   double cc[H], ss[H], tt[H];
-#pragma unroll
+HD_UNROLL_NN
   for (int k = 0; k < H; ++k) {
     const int x = tour_a(P, r, k), y = tour_b(P, r, k);
     const int p = x < y ? x : y, q = x < y ? y : x;
@@ -263,7 +270,7 @@ __device__ __forceinline__ void jacobi_round(int r, double (&a)[NN][NN], double 
     ss[k] = rot ? sg * apq * z : 0.0;
     tt[k] = rot ? sg * apq * (2.0 * w) * (z * z) : 0.0;
   }
-#pragma unroll
+HD_UNROLL_NN
   for (int k = 0; k < H; ++k) {
     const int x = tour_a(P, r, k), y = tour_b(P, r, k);
     const int p = x < y ? x : y, q = x < y ? y : x;
@@ -273,7 +280,7 @@ __device__ __forceinline__ void jacobi_round(int r, double (&a)[NN][NN], double 
     a[p][p] = fma(-t, apq, a[p][p]);
     a[q][q] = fma(t, apq, a[q][q]);
     a[p][q] = on ? 0.0 : apq;
-#pragma unroll
+HD_UNROLL_NN
     for (int i = 0; i < NN; ++i) {
       if (i == p || i == q) continue;
       const double aip = HD_SYM(a, i, p);
@@ -281,7 +288,7 @@ __device__ __forceinline__ void jacobi_round(int r, double (&a)[NN][NN], double 
       HD_SYM(a, i, p) = fma(c, aip, -s * aiq);
       HD_SYM(a, i, q) = fma(s, aip, c * aiq);
     }
-#pragma unroll
+HD_UNROLL_NN
     for (int i = 0; i < NN; ++i) {
       const double vip = v[i][p];
       const double viq = v[i][q];
@@ -298,23 +305,23 @@ __device__ __forceinline__ void jacobi_round(int r, double (&a)[NN][NN], double 
 template <int NN>
 __device__ __forceinline__ void jacobi_eig(double (&a)[NN][NN], double (&v)[NN][NN],
                                            int max_sweeps) {
-#pragma unroll
+HD_UNROLL_NN
   for (int i = 0; i < NN; ++i)
-#pragma unroll
+HD_UNROLL_NN
     for (int j = 0; j < NN; ++j) v[i][j] = (i == j) ? 1.0 : 0.0;
   if constexpr (NN > 1) {
     constexpr int P = NN + (NN & 1);
     for (int sweep = 0; sweep < max_sweeps; ++sweep) {
       double off = 0.0, dia = 0.0;
-#pragma unroll
+HD_UNROLL_NN
       for (int i = 0; i < NN; ++i) {
         dia = fma(a[i][i], a[i][i], dia);
-#pragma unroll
+HD_UNROLL_NN
         for (int j = i + 1; j < NN; ++j) off = fma(a[i][j], a[i][j], off);
       }
       const bool done = !(off > 1.0e-30 * dia);  // off-diagonal <~ 1e-15 relative
       if (__all(done)) break;
-#pragma unroll
+HD_UNROLL_NN
       for (int r = 0; r < P - 1; ++r) jacobi_round<NN>(r, a, v, !done);
     }
   }
@@ -337,13 +344,13 @@ __device__ __forceinline__ void jacobi_os_round(int r, double (&b)[NN][NN], doub
   constexpr int P = NN + (NN & 1);
   constexpr int H = P / 2;
   double cc[H], ss[H], gg[H];
-#pragma unroll
+HD_UNROLL_NN
   for (int k = 0; k < H; ++k) {
     const int x = tour_a(P, r, k), y = tour_b(P, r, k);
     const int p = x < y ? x : y, q = x < y ? y : x;
     if (q >= NN) continue;
     double g0 = 0.0, g1 = 0.0;  // two chains
-#pragma unroll
+HD_UNROLL_NN
     for (int i = 0; i < NN; ++i) {
       if (i % 2 == 0) g0 = fma(b[i][p], b[i][q], g0);
       else g1 = fma(b[i][p], b[i][q], g1);
@@ -364,13 +371,13 @@ __device__ __forceinline__ void jacobi_os_round(int r, double (&b)[NN][NN], doub
     ss[k] = rot ? sg * gam * z : 0.0;
     gg[k] = gam;
   }
-#pragma unroll
+HD_UNROLL_NN
   for (int k = 0; k < H; ++k) {
     const int x = tour_a(P, r, k), y = tour_b(P, r, k);
     const int p = x < y ? x : y, q = x < y ? y : x;
     if (q >= NN) continue;
     const double c = cc[k], s = ss[k];
-#pragma unroll
+HD_UNROLL_NN
     for (int i = 0; i < NN; ++i) {
       const double bp = b[i][p], bq = b[i][q];
       b[i][p] = fma(-s, bq, c * bp);
@@ -397,15 +404,15 @@ __device__ __forceinline__ void jacobi_os(double (&b)[NN][NN], int max_sweeps) {
     bool on = true;
     for (int sweep = 0; sweep < max_sweeps; ++sweep) {
       double nrm[NN], dia = 0.0, off = 0.0;
-#pragma unroll
+HD_UNROLL_NN
       for (int j = 0; j < NN; ++j) {
         double t = 0.0;
-#pragma unroll
+HD_UNROLL_NN
         for (int i = 0; i < NN; ++i) t = fma(b[i][j], b[i][j], t);
         nrm[j] = t;
         dia = fma(t, t, dia);
       }
-#pragma unroll
+HD_UNROLL_NN
       for (int r = 0; r < P - 1; ++r) jacobi_os_round<NN>(r, b, nrm, on, off);
       on = on && off > 1.0e-16 * dia;
       if (__all(!on)) break;

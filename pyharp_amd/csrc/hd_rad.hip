@@ -1,6 +1,6 @@
 // hd_rad.hip -- gfx950 kernels of the intensity path: every azimuthal mode,
 // fluxes at user optical depths (usrtau) and radiances at user angles
-// (usrang), nstr <= 16.  One lane owns one (solve, mode m) problem ("unit");
+// (usrang), nstr <= 32.  One lane owns one (solve, mode m) problem ("unit");
 // units are mode-major inside a chunk (u = m*ns + sl), so a wave's lanes share
 // m and the mode-m Legendre tables are uniform loads.
 //
@@ -29,11 +29,23 @@
 #include "hd_rad.hpp"
 
 namespace hd {
+#ifdef HD_RAD_WIDE
+namespace wide {
+#endif
 
 namespace {
 
 constexpr int kLayerBlockR = 256;
 constexpr int kLayersPerBlockR = kLayerBlockR / 64;
+
+// nstr <= 16 (NN <= 8, this translation unit): every NN-loop fully unrolled,
+// the matrices in registers.  nstr 18..32 (NN 9..16): hd_rad_wide.hip compiles
+// this same file with the NN-loops rolled (HD_RUNROLL = nounroll), so the
+// per-lane matrices live in private memory -- the coverage path of the
+// intensity kernels at large nstr (the flux path has the team kernels)
+#ifndef HD_RUNROLL
+#define HD_RUNROLL _Pragma("unroll")
+#endif
 
 template <int NN>
 struct RadTab {
@@ -63,6 +75,28 @@ struct RadConst {
 };
 __constant__ RadConst c_rad;
 
+#ifdef HD_RAD_WIDE
+struct RadConstWide {
+  Quad<9> q9;
+  Quad<10> q10;
+  Quad<11> q11;
+  Quad<12> q12;
+  Quad<13> q13;
+  Quad<14> q14;
+  Quad<15> q15;
+  Quad<16> q16;
+  RadTab<9> t9;
+  RadTab<10> t10;
+  RadTab<11> t11;
+  RadTab<12> t12;
+  RadTab<13> t13;
+  RadTab<14> t14;
+  RadTab<15> t15;
+  RadTab<16> t16;
+};
+__constant__ RadConstWide c_radw;
+#endif
+
 template <int NN>
 __device__ __forceinline__ const Quad<NN>& quad_r() {
   if constexpr (NN == 1) return c_rad.q1;
@@ -72,7 +106,17 @@ __device__ __forceinline__ const Quad<NN>& quad_r() {
   else if constexpr (NN == 5) return c_rad.q5;
   else if constexpr (NN == 6) return c_rad.q6;
   else if constexpr (NN == 7) return c_rad.q7;
-  else return c_rad.q8;
+  else if constexpr (NN == 8) return c_rad.q8;
+#ifdef HD_RAD_WIDE
+  else if constexpr (NN == 9) return c_radw.q9;
+  else if constexpr (NN == 10) return c_radw.q10;
+  else if constexpr (NN == 11) return c_radw.q11;
+  else if constexpr (NN == 12) return c_radw.q12;
+  else if constexpr (NN == 13) return c_radw.q13;
+  else if constexpr (NN == 14) return c_radw.q14;
+  else if constexpr (NN == 15) return c_radw.q15;
+  else return c_radw.q16;
+#endif
 }
 template <int NN>
 __device__ __forceinline__ const RadTab<NN>& tab_r() {
@@ -83,7 +127,17 @@ __device__ __forceinline__ const RadTab<NN>& tab_r() {
   else if constexpr (NN == 5) return c_rad.t5;
   else if constexpr (NN == 6) return c_rad.t6;
   else if constexpr (NN == 7) return c_rad.t7;
-  else return c_rad.t8;
+  else if constexpr (NN == 8) return c_rad.t8;
+#ifdef HD_RAD_WIDE
+  else if constexpr (NN == 9) return c_radw.t9;
+  else if constexpr (NN == 10) return c_radw.t10;
+  else if constexpr (NN == 11) return c_radw.t11;
+  else if constexpr (NN == 12) return c_radw.t12;
+  else if constexpr (NN == 13) return c_radw.t13;
+  else if constexpr (NN == 14) return c_radw.t14;
+  else if constexpr (NN == 15) return c_radw.t15;
+  else return c_radw.t16;
+#endif
 }
 
 // Y_m^m(x) = seed_m (1 - x^2)^(m/2)
@@ -188,7 +242,12 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
   constexpr int N = 2 * NN;
   constexpr int kPsi = NN > 1 ? NN * NN : 1;
   constexpr int nsym = NN * (NN + 1) / 2;
-  __shared__ double psi_lds[kPsi * kLayerBlockR];
+  __shared__ double psi_lds[NN <= 8 ? kPsi * kLayerBlockR : 1];
+  double psi_priv[NN <= 8 ? 1 : kPsi];  // NN > 8: private memory, like the matrices
+  auto psi_at = [&](int e) -> double& {
+    if constexpr (NN <= 8) return psi_lds[e * kLayerBlockR + threadIdx.x];
+    else return psi_priv[e];
+  };
   const Quad<NN>& Qc = quad_r<NN>();
   const int lt = threadIdx.x;
   const int ntile = (A.nu + 63) / 64;
@@ -227,10 +286,10 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
 
   // ---- mode-m phase matrix even/odd parts (parity of l+m) + beam vectors ----
   double lch[NN][NN], ap[NN][NN], xs[NN], xd[NN];
-#pragma unroll
+HD_RUNROLL
   for (int i = 0; i < NN; ++i) {
     xs[i] = xd[i] = 0.0;
-#pragma unroll
+HD_RUNROLL
     for (int j = i; j < NN; ++j) lch[i][j] = ap[i][j] = 0.0;
   }
   {
@@ -258,25 +317,25 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
       const double* te = lam + le * NN;
       const double* to = lam + lo * NN;
       double ue[NN], uo[NN];
-#pragma unroll
+HD_RUNROLL
       for (int i = 0; i < NN; ++i) {
         ue[i] = ge * te[i];
         uo[i] = go * to[i];
         xs[i] = fma(ue[i], pe0, xs[i]);
         xd[i] = fma(uo[i], po0, xd[i]);
       }
-#pragma unroll
+HD_RUNROLL
       for (int i = 0; i < NN; ++i)
-#pragma unroll
+HD_RUNROLL
         for (int j = i; j < NN; ++j) {
           ap[i][j] = fma(ue[i], te[j], ap[i][j]);
           lch[i][j] = fma(uo[i], to[j], lch[i][j]);
         }
     }
   }
-#pragma unroll
+HD_RUNROLL
   for (int i = 0; i < NN; ++i)
-#pragma unroll
+HD_RUNROLL
     for (int j = i; j < NN; ++j) {
       const double diag = (i == j) ? Qc.rmu[i] : 0.0;
       const double sij = Qc.sd[i] * Qc.sd[j];
@@ -295,23 +354,23 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
   const double fb2 = fb * ((m == 0 ? 0.5 : 1.0) / kPi);
   if (beam) {
     double y[NN], z[NN];
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) y[i] = Qc.sd[i] * (fb2 * xs[i]);
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) {
       double t = 0.0;
-#pragma unroll
+HD_RUNROLL
       for (int k = i; k < NN; ++k) t = fma(lch[k][i], y[k], t);
       z[i] = t;
     }
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) {
       double t = 0.0;
-#pragma unroll
+HD_RUNROLL
       for (int k = 0; k <= i; ++k) t = fma(lch[i][k], z[k], t);
       y[i] = t;
     }
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) {
       const double xdi = -fb2 * xd[i];
       const double rv = fma(-y[i], Qc.rg[i], xdi * rmu0 * Qc.rmu[i]);
@@ -323,7 +382,7 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
     lower_solve<NN>(lch, rdl, lxd);
     lower_t_solve<NN>(lch, rdl, lxd);
   } else {
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) y2[i] = lxd[i] = 0.0;
   }
   // thermal (m = 0): cvec = dB + 2 (dB/tau') h,  h = W^-1 D^1/2 L^-T L^-1 D^1/2 mu
@@ -335,11 +394,11 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
     db = bb - bt;
     bsum = bt + bb;
     const double b1 = taup > 0.0 ? 2.0 * db / taup : 0.0;
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) cvec[i] = Qc.sd[i] * Qc.mu[i];
     lower_solve<NN>(lch, rdl, cvec);
     lower_t_solve<NN>(lch, rdl, cvec);
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) {
       rr[(oH + i) * nu] = Qc.rg[i] * cvec[i];
       cvec[i] = fma(b1 * Qc.rg[i], cvec[i], db);
@@ -347,7 +406,7 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
     rr[oBt * nu] = bt;
     rr[oSl * nu] = 0.5 * b1;
   } else {
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) {
       cvec[i] = 0.0;
       rr[(oH + i) * nu] = 0.0;
@@ -359,9 +418,9 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
   rr[oOm * nu] = om;
   {  // L (packed lower, row-major)
     int e = 0;
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i)
-#pragma unroll
+HD_RUNROLL
       for (int k = 0; k <= i; ++k) rr[(e++) * nu] = lch[i][k];
   }
 
@@ -371,33 +430,33 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
   double rdc[NN];
   if (!chol_inplace<NN>(ap, rdc)) st |= kStEigen;  // lower ap <- C
   double v[NN][NN];  // B, then U = L V, then Omega = U Delta^1/2
-#pragma unroll
+HD_RUNROLL
   for (int i = 0; i < NN; ++i)
-#pragma unroll
+HD_RUNROLL
     for (int j = 0; j < NN; ++j) {  // B_ij = sum_{k >= max(i,j)} C_ki L_kj
       double t = 0.0;
-#pragma unroll
+HD_RUNROLL
       for (int k = (i > j ? i : j); k < NN; ++k) t = fma(ap[k][i], lch[k][j], t);
       v[i][j] = t;
     }
   jacobi_os<NN>(v, A.max_sweeps);
   double kk[NN];
-#pragma unroll
+HD_RUNROLL
   for (int j = 0; j < NN; ++j) {
     double k2 = 0.0;
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) k2 = fma(v[i][j], v[i][j], k2);
     if (!(k2 > 0.0)) st |= kStEigen;
     kk[j] = sqrt(k2 > 0.0 ? k2 : 0.0);
     rr[(oK + j) * nu] = kk[j];
   }
-#pragma unroll
+HD_RUNROLL
   for (int j = 0; j < NN; ++j) {  // U = C^-T B, column by column
     double x[NN];
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) x[i] = v[i][j];
     lower_t_solve<NN>(ap, rdc, x);
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) v[i][j] = x[i];
   }
 
@@ -407,10 +466,10 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
   if (beam) {
     double tt[NN];
     const double r2 = rmu0 * rmu0;
-#pragma unroll
+HD_RUNROLL
     for (int j = 0; j < NN; ++j) {  // tt = V^T y2 / (1/mu0^2 - k^2), V^T y2 = U^T (L^-T y2)
       double t = 0.0;
-#pragma unroll
+HD_RUNROLL
       for (int i = 0; i < NN; ++i) t = fma(v[i][j], y2[i], t);
       double den = fma(-kk[j], kk[j], r2);
       if (fabs(den) < 1.0e-9 * r2) {
@@ -420,20 +479,20 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
       tt[j] = t / den;
     }
     double sv[NN], y[NN];
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) {  // s = W^-1 D^1/2 L V tt = W^-1 D^1/2 U tt
       double t = 0.0;
-#pragma unroll
+HD_RUNROLL
       for (int j = 0; j < NN; ++j) t = fma(v[i][j], tt[j], t);
       sv[i] = Qc.rg[i] * t;
     }
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) y[i] = Qc.sd[i] * Qc.mu[i] * sv[i];
     lower_solve<NN>(lch, rdl, y);
     lower_t_solve<NN>(lch, rdl, y);
     const double tauc = A.tauc[(size_t)lc * A.ns + sl];
     const double att = 0.5 * exp(-tauc * rmu0);
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) {
       const double dd = Qc.rg[i] * fma(-y[i], rmu0, lxd[i]);
       zp[i] = (sv[i] + dd) * att;
@@ -441,10 +500,10 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
     }
     e0 = exp(-taup * rmu0);
   } else {
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) zp[i] = zm[i] = 0.0;
   }
-#pragma unroll
+HD_RUNROLL
   for (int i = 0; i < NN; ++i) {
     rr[(oZp + i) * nu] = zp[i];
     rr[(oZm + i) * nu] = zm[i];
@@ -452,7 +511,7 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
 
   // ---- layer operators in the flux-weighted basis (as hd_layer_kernel) ----
   double dsq[NN], gsq[NN];
-#pragma unroll
+HD_RUNROLL
   for (int j = 0; j < NN; ++j) {
     const double x = kk[j] * taup;
     const double mm = -expm1(-x);
@@ -463,26 +522,26 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
     rr[(oEk + j) * nu] = 1.0 - mm;  // exp(-k tau') for the user-angle kernel
   }
   rr[oE0 * nu] = e0;
-#pragma unroll
+HD_RUNROLL
   for (int j = 0; j < NN; ++j) {  // V = L^-1 U (stored), Psi^T = L^-T V Gamma^1/2 -> LDS
     double x[NN];
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) x[i] = v[i][j];
     lower_solve<NN>(lch, rdl, x);
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) rr[(oV + i * NN + j) * nu] = x[i];
     lower_t_solve<NN>(lch, rdl, x);
-#pragma unroll
-    for (int i = 0; i < NN; ++i) psi_lds[(i * NN + j) * kLayerBlockR + lt] = x[i] * gsq[j];
+HD_RUNROLL
+    for (int i = 0; i < NN; ++i) psi_at(i * NN + j) = x[i] * gsq[j];
   }
-#pragma unroll
+HD_RUNROLL
   for (int i = 0; i < NN; ++i)  // Omega = L V Delta^1/2 = U Delta^1/2
-#pragma unroll
+HD_RUNROLL
     for (int j = 0; j < NN; ++j) v[i][j] *= dsq[j];
 
   double* out = A.rsw + (size_t)lc * ne1<NN>() * nu + u;
   double ga[NN], gb[NN];
-#pragma unroll
+HD_RUNROLL
   for (int i = 0; i < NN; ++i) {
     ga[i] = Qc.g[i] * (cvec[i] - fma(-zp[i], e0, zm[i]));
     gb[i] = Qc.g[i] * (fma(zp[i], e0, zm[i]) + bsum);
@@ -491,22 +550,22 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
   // A- = (I + Omega Omega^T)^-1, A+ = (I + Psi^T Psi)^-1; R~ = A+ - A-, T~ = A- + A+ - I
   double pvec[NN], am_[NN][NN];
   {
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i)
-#pragma unroll
+HD_RUNROLL
       for (int j = i; j < NN; ++j) {
         double t = (i == j) ? 1.0 : 0.0;
-#pragma unroll
+HD_RUNROLL
         for (int k = 0; k < NN; ++k) t = fma(v[i][k], v[j][k], t);
         am_[i][j] = t;
       }
     double rdh[NN];
     if (!chol_inplace<NN>(am_, rdh)) st |= kStEigen;
     spd_inverse_upper<NN>(am_, rdh);
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) {  // p = Q~- ga = ga - A- ga
       double t = ga[i];
-#pragma unroll
+HD_RUNROLL
       for (int j = 0; j < NN; ++j) t = fma(-HD_SYM(am_, i, j), ga[j], t);
       pvec[i] = t;
     }
@@ -514,26 +573,26 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
   double ap_[NN][NN], qvec[NN];
   {
     double pt_[NN][NN];  // pt_[i][j] = Psi^T[i][j]
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i)
-#pragma unroll
-      for (int j = 0; j < NN; ++j) pt_[i][j] = psi_lds[(i * NN + j) * kLayerBlockR + lt];
-#pragma unroll
+HD_RUNROLL
+      for (int j = 0; j < NN; ++j) pt_[i][j] = psi_at(i * NN + j);
+HD_RUNROLL
     for (int i = 0; i < NN; ++i)
-#pragma unroll
+HD_RUNROLL
       for (int j = i; j < NN; ++j) {
         double t = (i == j) ? 1.0 : 0.0;
-#pragma unroll
+HD_RUNROLL
         for (int k = 0; k < NN; ++k) t = fma(pt_[i][k], pt_[j][k], t);
         ap_[i][j] = t;
       }
     double rdh[NN];
     if (!chol_inplace<NN>(ap_, rdh)) st |= kStEigen;
     spd_inverse_upper<NN>(ap_, rdh);
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) {  // q = Q~+ gb = A+ gb - gb
       double t = -gb[i];
-#pragma unroll
+HD_RUNROLL
       for (int j = 0; j < NN; ++j) t = fma(HD_SYM(ap_, i, j), gb[j], t);
       qvec[i] = t;
     }
@@ -541,9 +600,9 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
   double chk = 0.0;
   {
     int e = 0;
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i)
-#pragma unroll
+HD_RUNROLL
       for (int j = i; j < NN; ++j) {
         const double r = ap_[i][j] - am_[i][j];
         const double t = (am_[i][j] + ap_[i][j]) - ((i == j) ? 1.0 : 0.0);
@@ -553,7 +612,7 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
         ++e;
       }
   }
-#pragma unroll
+HD_RUNROLL
   for (int i = 0; i < NN; ++i) {
     const double sp = Qc.g[i] * (zp[i] * (1.0 - e0) - db) + pvec[i] - qvec[i];
     const double sm = Qc.g[i] * (-zm[i] * (1.0 - e0) + db) - pvec[i] - qvec[i];
@@ -600,10 +659,10 @@ __global__ __launch_bounds__(64) void hd_rad_sweep_kernel(RadArgs A) {
 
   double ra[NN][NN];
   double sd[NN];
-#pragma unroll
+HD_RUNROLL
   for (int i = 0; i < NN; ++i) {
     sd[i] = Qc.g[i] * top;
-#pragma unroll
+HD_RUNROLL
     for (int j = i; j < NN; ++j) ra[i][j] = 0.0;
   }
   double tauc = 0.0;
@@ -612,88 +671,88 @@ __global__ __launch_bounds__(64) void hd_rad_sweep_kernel(RadArgs A) {
     double* bp = A.bsub + (size_t)lc * NB * nu + u;
     {  // stack above this layer: R_above (packed upper) and S_down
       int e = 0;
-#pragma unroll
+HD_RUNROLL
       for (int i = 0; i < NN; ++i)
-#pragma unroll
+HD_RUNROLL
         for (int j = i; j < NN; ++j) bp[(NN * NN + NN + (e++)) * nu] = ra[i][j];
-#pragma unroll
+HD_RUNROLL
       for (int i = 0; i < NN; ++i) bp[(NN * NN + NN + nsym + i) * nu] = sd[i];
     }
     double rl[NN][NN], spl[NN];
     {
       int e = 0;
-#pragma unroll
+HD_RUNROLL
       for (int i = 0; i < NN; ++i)
-#pragma unroll
+HD_RUNROLL
         for (int j = i; j < NN; ++j) rl[i][j] = lp[(size_t)(e++) * nu];
-#pragma unroll
+HD_RUNROLL
       for (int i = 0; i < NN; ++i) spl[i] = lp[(size_t)(2 * nsym + i) * nu];
     }
     double am[NN][NN], w1[NN][NN], t1[NN];
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i)
-#pragma unroll
+HD_RUNROLL
       for (int j = 0; j < NN; ++j) am[i][j] = HD_SYM(ra, i, j);
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) {
-#pragma unroll
+HD_RUNROLL
       for (int j = 0; j < NN; ++j) {
         double t = (i == j) ? 1.0 : 0.0;
-#pragma unroll
+HD_RUNROLL
         for (int k = 0; k < NN; ++k) t = fma(-HD_SYM(rl, i, k), am[k][j], t);
         w1[i][j] = t;
       }
       double t = spl[i];
-#pragma unroll
+HD_RUNROLL
       for (int k = 0; k < NN; ++k) t = fma(HD_SYM(rl, i, k), sd[k], t);
       t1[i] = t;
     }
-#pragma unroll
+HD_RUNROLL
     for (int k = 0; k < NN; ++k) {
       const double piv = w1[k][k];
       if (!(fabs(piv) > 1.0e-12)) st |= kStPivot;
       const double rp = rcp_nr(piv);
       w1[k][k] = rp;
-#pragma unroll
+HD_RUNROLL
       for (int i = k + 1; i < NN; ++i) {
         const double l = w1[i][k] * rp;
         w1[i][k] = l;
-#pragma unroll
+HD_RUNROLL
         for (int j = k + 1; j < NN; ++j) w1[i][j] = fma(-l, w1[k][j], w1[i][j]);
       }
     }
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i)
-#pragma unroll
+HD_RUNROLL
       for (int k = 0; k < i; ++k) t1[i] = fma(-w1[i][k], t1[k], t1[i]);
-#pragma unroll
+HD_RUNROLL
     for (int i = NN - 1; i >= 0; --i) {
-#pragma unroll
+HD_RUNROLL
       for (int k = i + 1; k < NN; ++k) t1[i] = fma(-w1[i][k], t1[k], t1[i]);
       t1[i] *= w1[i][i];
     }
     double uvec[NN];
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) {
       double t = sd[i];
-#pragma unroll
+HD_RUNROLL
       for (int k = 0; k < NN; ++k) t = fma(am[i][k], t1[k], t);
       uvec[i] = t;
       bp[(size_t)(NN * NN + i) * nu] = t1[i];
     }
-#pragma unroll
+HD_RUNROLL
     for (int r = 0; r < NN; ++r) {
-#pragma unroll
+HD_RUNROLL
       for (int j = 0; j < NN; ++j) {
         double t = am[r][j];
-#pragma unroll
+HD_RUNROLL
         for (int k = 0; k < j; ++k) t = fma(-am[r][k], w1[k][j], t);
         am[r][j] = t * w1[j][j];
       }
-#pragma unroll
+HD_RUNROLL
       for (int j = NN - 1; j >= 0; --j) {
         double t = am[r][j];
-#pragma unroll
+HD_RUNROLL
         for (int k = j + 1; k < NN; ++k) t = fma(-am[r][k], w1[k][j], t);
         am[r][j] = t;
       }
@@ -701,53 +760,53 @@ __global__ __launch_bounds__(64) void hd_rad_sweep_kernel(RadArgs A) {
     double tl[NN][NN];
     {
       int e = nsym;
-#pragma unroll
+HD_RUNROLL
       for (int i = 0; i < NN; ++i)
-#pragma unroll
+HD_RUNROLL
         for (int j = i; j < NN; ++j) tl[i][j] = lp[(size_t)(e++) * nu];
     }
-#pragma unroll
+HD_RUNROLL
     for (int j = 0; j < NN; ++j) {
       double x[NN];
-#pragma unroll
+HD_RUNROLL
       for (int i = 0; i < NN; ++i) x[i] = HD_SYM(tl, i, j);
-#pragma unroll
+HD_RUNROLL
       for (int i = 0; i < NN; ++i)
-#pragma unroll
+HD_RUNROLL
         for (int k = 0; k < i; ++k) x[i] = fma(-w1[i][k], x[k], x[i]);
-#pragma unroll
+HD_RUNROLL
       for (int i = NN - 1; i >= 0; --i) {
-#pragma unroll
+HD_RUNROLL
         for (int k = i + 1; k < NN; ++k) x[i] = fma(-w1[i][k], x[k], x[i]);
         x[i] *= w1[i][i];
       }
-#pragma unroll
+HD_RUNROLL
       for (int i = 0; i < NN; ++i) bp[(size_t)(i * NN + j) * nu] = x[i];
     }
-#pragma unroll
+HD_RUNROLL
     for (int r = 0; r < NN; ++r) {
       double row[NN];
-#pragma unroll
+HD_RUNROLL
       for (int j = 0; j < NN; ++j) {
         double t = 0.0;
-#pragma unroll
+HD_RUNROLL
         for (int k = 0; k < NN; ++k) t = fma(am[r][k], HD_SYM(tl, k, j), t);
         row[j] = t;
       }
-#pragma unroll
+HD_RUNROLL
       for (int j = 0; j < NN; ++j) am[r][j] = row[j];
     }
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) {
-#pragma unroll
+HD_RUNROLL
       for (int j = i; j < NN; ++j) {
         double t = rl[i][j];
-#pragma unroll
+HD_RUNROLL
         for (int k = 0; k < NN; ++k) t = fma(HD_SYM(tl, i, k), am[k][j], t);
         ra[i][j] = t;
       }
       double t = lp[(size_t)(2 * nsym + NN + i) * nu];
-#pragma unroll
+HD_RUNROLL
       for (int k = 0; k < NN; ++k) t = fma(HD_SYM(tl, i, k), uvec[k], t);
       sd[i] = t;
     }
@@ -756,10 +815,10 @@ __global__ __launch_bounds__(64) void hd_rad_sweep_kernel(RadArgs A) {
 
   // ---- Lambertian surface (mode 0): I+ = x for every stream ----
   double gsd = 0.0, grg = 0.0;
-#pragma unroll
+HD_RUNROLL
   for (int i = 0; i < NN; ++i) {
     gsd += Qc.g[i] * sd[i];
-#pragma unroll
+HD_RUNROLL
     for (int j = 0; j < NN; ++j) grg += Qc.g[i] * HD_SYM(ra, i, j) * Qc.g[j];
   }
   double esurf = (1.0 - alb) * bsurf;
@@ -769,12 +828,12 @@ __global__ __launch_bounds__(64) void hd_rad_sweep_kernel(RadArgs A) {
   double chk = 0.0;
   {
     double* lv = A.lev + (size_t)L * 2 * NN * nu + u;
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) ip[i] = Qc.g[i] * x;
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) {
       double t = sd[i];
-#pragma unroll
+HD_RUNROLL
       for (int j = 0; j < NN; ++j) t = fma(HD_SYM(ra, i, j), ip[j], t);
       lv[i * nu] = x;
       lv[(NN + i) * nu] = t * Qc.rg[i];
@@ -785,29 +844,29 @@ __global__ __launch_bounds__(64) void hd_rad_sweep_kernel(RadArgs A) {
   for (int lc = L - 1; lc >= 0; --lc) {
     const double* bp = A.bsub + (size_t)lc * NB * nu + u;
     double nip[NN];
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) {
       double t = bp[(size_t)(NN * NN + i) * nu];
-#pragma unroll
+HD_RUNROLL
       for (int j = 0; j < NN; ++j) t = fma(bp[(size_t)(i * NN + j) * nu], ip[j], t);
       nip[i] = t;
     }
     double* lv = A.lev + (size_t)lc * 2 * NN * nu + u;
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) ip[i] = nip[i];
     int e = 0;
     double dn[NN];
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) dn[i] = bp[(size_t)(NN * NN + NN + nsym + i) * nu];
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i)
-#pragma unroll
+HD_RUNROLL
       for (int j = i; j < NN; ++j) {
         const double r = bp[(size_t)(NN * NN + NN + (e++)) * nu];
         dn[i] = fma(r, ip[j], dn[i]);
         if (j != i) dn[j] = fma(r, ip[i], dn[j]);
       }
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) {
       lv[i * nu] = ip[i] * Qc.rg[i];
       lv[(NN + i) * nu] = dn[i] * Qc.rg[i];
@@ -831,17 +890,17 @@ __device__ __forceinline__ void load_layer(const RadArgs& A, int lc, int u, doub
   const size_t nu = A.nu;
   const double* rr = A.rrd + (size_t)lc * rad_rec_doubles(NN) * nu + u;
   int e = 0;
-#pragma unroll
+HD_RUNROLL
   for (int i = 0; i < NN; ++i)
-#pragma unroll
+HD_RUNROLL
     for (int k = 0; k <= i; ++k) lch[i][k] = rr[(e++) * nu];
-#pragma unroll
+HD_RUNROLL
   for (int i = 0; i < NN; ++i) rd[i] = 1.0 / lch[i][i];
-#pragma unroll
+HD_RUNROLL
   for (int i = 0; i < NN; ++i)
-#pragma unroll
+HD_RUNROLL
     for (int j = 0; j < NN; ++j) v[i][j] = rr[(nsym + i * NN + j) * nu];
-#pragma unroll
+HD_RUNROLL
   for (int j = 0; j < NN; ++j) kk[j] = rr[(nsym + NN * NN + j) * nu];
 }
 
@@ -866,14 +925,14 @@ __global__ __launch_bounds__(256) void hd_rad_const_kernel(RadArgs A) {
   const double fb = A.fbeam ? A.fbeam[s] : 0.0;
   const double rmu0 = (fb > 0.0 && mu0 > 0.0) ? 1.0 / mu0 : 0.0;
   double cp[NN], cm[NN];
-#pragma unroll
+HD_RUNROLL
   for (int side = 0; side < 2; ++side) {  // 0: layer top, 1: layer bottom
     const double t = side ? taup : 0.0;
     const double eb = exp(-t * rmu0);
     const double b2 = 2.0 * fma(slope, t, bt);
     const double* lv = A.lev + (size_t)(lc + side) * 2 * NN * nu + u;
     double xs[NN], yd[NN];
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) {
       const double ipl = lv[i * nu], imi = lv[(NN + i) * nu];
       const double zp = rr[(oZp + i) * nu], zm = rr[(oZm + i) * nu], h = rr[(oH + i) * nu];
@@ -882,17 +941,17 @@ __global__ __launch_bounds__(256) void hd_rad_const_kernel(RadArgs A) {
     }
     lower_solve<NN>(lch, rd, xs);
     double ly[NN];
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) {  // L^T yd
       double a = 0.0;
-#pragma unroll
+HD_RUNROLL
       for (int k = i; k < NN; ++k) a = fma(lch[k][i], yd[k], a);
       ly[i] = a;
     }
-#pragma unroll
+HD_RUNROLL
     for (int j = 0; j < NN; ++j) {
       double a = 0.0, b = 0.0;
-#pragma unroll
+HD_RUNROLL
       for (int i = 0; i < NN; ++i) {
         a = fma(v[i][j], xs[i], a);
         b = fma(v[i][j], ly[i], b);
@@ -903,7 +962,7 @@ __global__ __launch_bounds__(256) void hd_rad_const_kernel(RadArgs A) {
     }
   }
   double* co = A.cst + (size_t)lc * 2 * NN * nu + u;
-#pragma unroll
+HD_RUNROLL
   for (int j = 0; j < NN; ++j) {
     co[j * nu] = cp[j];
     co[(NN + j) * nu] = cm[j];
@@ -943,7 +1002,7 @@ __global__ __launch_bounds__(256) void hd_rad_flux_kernel(RadArgs A) {
   const double rmu0 = beam ? 1.0 / mu0 : 0.0;
   const double* co = A.cst + (size_t)lc * 2 * NN * nu + u;
   double al[NN], be[NN];
-#pragma unroll
+HD_RUNROLL
   for (int j = 0; j < NN; ++j) {
     const double a = co[j * nu] * exp(-kk[j] * t);
     const double b = co[(NN + j) * nu] * exp(-kk[j] * (taup - t));
@@ -951,10 +1010,10 @@ __global__ __launch_bounds__(256) void hd_rad_flux_kernel(RadArgs A) {
     be[j] = kk[j] * (a - b);
   }
   double gs[NN], gd[NN];
-#pragma unroll
+HD_RUNROLL
   for (int i = 0; i < NN; ++i) {  // V al, V (k be)
     double a = 0.0, b = 0.0;
-#pragma unroll
+HD_RUNROLL
     for (int j = 0; j < NN; ++j) {
       a = fma(v[i][j], al[j], a);
       b = fma(v[i][j], be[j], b);
@@ -962,10 +1021,10 @@ __global__ __launch_bounds__(256) void hd_rad_flux_kernel(RadArgs A) {
     gs[i] = a;
     gd[i] = b;
   }
-#pragma unroll
+HD_RUNROLL
   for (int i = NN - 1; i >= 0; --i) {  // gs <- L gs (rows bottom-up, in place)
     double a = 0.0;
-#pragma unroll
+HD_RUNROLL
     for (int k = 0; k <= i; ++k) a = fma(lch[i][k], gs[k], a);
     gs[i] = a;
   }
@@ -973,7 +1032,7 @@ __global__ __launch_bounds__(256) void hd_rad_flux_kernel(RadArgs A) {
   const double eb = exp(-t * rmu0);
   const double bb = fma(slope, t, bt);
   double up = 0.0, dn = 0.0;
-#pragma unroll
+HD_RUNROLL
   for (int i = 0; i < NN; ++i) {
     const double zp = rr[(oZp + i) * nu], zm = rr[(oZm + i) * nu], h = rr[(oH + i) * nu];
     const double ipl = 0.5 * (gs[i] - gd[i]) + Qc.g[i] * (zp * eb + bb + slope * h);
@@ -1022,7 +1081,7 @@ __global__ __launch_bounds__(64) void hd_rad_user_kernel(RadArgs A) {
   double yu[N], y0[N];
   ylm_row<N>(m, muu, yu);
   ylm_row<N>(m, beam ? mu0 : 0.0, y0);
-#pragma unroll
+HD_RUNROLL
   for (int l = 0; l < N; ++l) y0[l] = ((l + m) & 1) ? -y0[l] : y0[l];  // Y_l^m(-mu0)
   const double* lam = &tab_r<NN>().lam[m][0][0];
   const bool up = muu > 0.0;
@@ -1033,7 +1092,7 @@ __global__ __launch_bounds__(64) void hd_rad_user_kernel(RadArgs A) {
     if (m == 0) {
       const double* lv = A.lev + (size_t)L * 2 * NN * nu + u;
       double fdn = 0.0;
-#pragma unroll
+HD_RUNROLL
       for (int i = 0; i < NN; ++i) fdn = fma(Qc.g[i] * Qc.g[i], lv[(NN + i) * nu], fdn);
       fdn *= 2.0 * kPi;
       const double alb = A.albedo ? A.albedo[s] : 0.0;
@@ -1068,7 +1127,7 @@ __global__ __launch_bounds__(64) void hd_rad_user_kernel(RadArgs A) {
     double cue[NN], cuo[NN];
     double x0 = 0.0;
     double gy[N];
-#pragma unroll
+HD_RUNROLL
     for (int l = 0; l < N; ++l) {
       const double chi = l == 0 ? 1.0 : (l <= nm ? q[1 + l] : 0.0);
       const double gl = (2 * l + 1) * (chi - f) * rf;
@@ -1077,10 +1136,10 @@ __global__ __launch_bounds__(64) void hd_rad_user_kernel(RadArgs A) {
     }
     // even/odd parts in l + m: m is uniform per block, so is the branch
     auto lsum = [&](int par) {
-#pragma unroll
+HD_RUNROLL
       for (int i = 0; i < NN; ++i) {
         double e = 0.0, o = 0.0;
-#pragma unroll
+HD_RUNROLL
         for (int l2 = 0; l2 < NN; ++l2) {
           e = fma(gy[2 * l2 + par], lam[(2 * l2 + par) * NN + i], e);
           o = fma(gy[2 * l2 + 1 - par], lam[(2 * l2 + 1 - par) * NN + i], o);
@@ -1096,17 +1155,17 @@ __global__ __launch_bounds__(64) void hd_rad_user_kernel(RadArgs A) {
     // ce = V^T L^T (sd cue), co = -k V^T L^-1 (sd cuo); L and V streamed from the
     // record (each element used once), not held in registers
     double a1[NN], b1[NN];
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) {
       a1[i] = 0.0;
       b1[i] = Qc.sd[i] * cuo[i];
     }
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i) {  // row i of L: a1 += L[i][:]^T (sd cue)_i ; b1 forward subst.
       const double* li = rr + (size_t)(i * (i + 1) / 2) * nu;
       const double ce_i = Qc.sd[i] * cue[i];
       double t = b1[i];
-#pragma unroll
+HD_RUNROLL
       for (int k2 = 0; k2 < i; ++k2) {
         const double l = li[k2 * nu];
         a1[k2] = fma(l, ce_i, a1[k2]);
@@ -1119,20 +1178,20 @@ __global__ __launch_bounds__(64) void hd_rad_user_kernel(RadArgs A) {
     const double* co = A.cst + (size_t)lc * 2 * NN * nu + u;
     const double* vr = rr + (size_t)nsym * nu;
     double kk[NN], hpl[NN], hmi[NN];
-#pragma unroll
+HD_RUNROLL
     for (int j = 0; j < NN; ++j) {
       hpl[j] = hmi[j] = 0.0;
       kk[j] = rr[(nsym + NN * NN + j) * nu];
     }
-#pragma unroll
+HD_RUNROLL
     for (int i = 0; i < NN; ++i)
-#pragma unroll
+HD_RUNROLL
       for (int j = 0; j < NN; ++j) {
         const double vij = vr[(i * NN + j) * nu];
         hpl[j] = fma(vij, a1[i], hpl[j]);  // ce
         hmi[j] = fma(vij, b1[i], hmi[j]);  // V^T b1
       }
-#pragma unroll
+HD_RUNROLL
     for (int j = 0; j < NN; ++j) {
       const double ce = hpl[j], cx = -kk[j] * hmi[j];
       hpl[j] = co[j * nu] * (ce + cx);
@@ -1141,7 +1200,7 @@ __global__ __launch_bounds__(64) void hd_rad_user_kernel(RadArgs A) {
     double ab = 0.0, a0 = 0.0, a1t = 0.0;
     if (beam) {
       double sc = 0.0;
-#pragma unroll
+HD_RUNROLL
       for (int i = 0; i < NN; ++i) {
         const double zp = rr[(oZp + i) * nu], zm = rr[(oZm + i) * nu];
         sc = fma(Qc.w[i], fma(cue[i], zp + zm, cuo[i] * (zp - zm)), sc);
@@ -1150,7 +1209,7 @@ __global__ __launch_bounds__(64) void hd_rad_user_kernel(RadArgs A) {
     }
     if (therm) {
       double we = 0.0, wo = 0.0;
-#pragma unroll
+HD_RUNROLL
       for (int i = 0; i < NN; ++i) {
         we = fma(Qc.w[i], cue[i], we);
         wo = fma(Qc.w[i] * cuo[i], rr[(oH + i) * nu], wo);
@@ -1162,7 +1221,7 @@ __global__ __launch_bounds__(64) void hd_rad_user_kernel(RadArgs A) {
     // general segment [t1 (evaluation), t2 (far end)] for user depths inside the layer
     auto integ = [&](double t1, double t2) {
       double r = 0.0;
-#pragma unroll
+HD_RUNROLL
       for (int j = 0; j < NN; ++j) {
         r += seg_exp(hpl[j], kk[j], t1, t2, 0.0, muu);
         r += seg_exp(hmi[j], -kk[j], t1, t2, taup, muu);
@@ -1182,7 +1241,7 @@ __global__ __launch_bounds__(64) void hd_rad_user_kernel(RadArgs A) {
     const double lmu = taup / anu;
     const double emu = exp(-lmu);
     double lay = 0.0;
-#pragma unroll
+HD_RUNROLL
     for (int j = 0; j < NN; ++j) {
       const double ek = rr[(oEk + j) * nu];
       const double reg = (1.0 - ek * emu) / fma(kk[j], anu, 1.0);
@@ -1383,6 +1442,23 @@ hipError_t upload_rad_tables(const QuadHost* per_nn) {
   fill_rad<6>(c.q6, c.t6, per_nn[5]);
   fill_rad<7>(c.q7, c.t7, per_nn[6]);
   fill_rad<8>(c.q8, c.t8, per_nn[7]);
+#ifdef HD_RAD_WIDE
+  static RadConstWide cw;  // ~560 KB
+  fill_rad<9>(cw.q9, cw.t9, per_nn[8]);
+  fill_rad<10>(cw.q10, cw.t10, per_nn[9]);
+  fill_rad<11>(cw.q11, cw.t11, per_nn[10]);
+  fill_rad<12>(cw.q12, cw.t12, per_nn[11]);
+  fill_rad<13>(cw.q13, cw.t13, per_nn[12]);
+  fill_rad<14>(cw.q14, cw.t14, per_nn[13]);
+  fill_rad<15>(cw.q15, cw.t15, per_nn[14]);
+  fill_rad<16>(cw.q16, cw.t16, per_nn[15]);
+  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_radw), &cw, sizeof(RadConstWide));
+  if (e != hipSuccess) return e;
+#else
+  // the nstr 18..32 instantiations keep their own tables (hd_rad_wide.hip)
+  hipError_t e = wide::upload_rad_tables(per_nn);
+  if (e != hipSuccess) return e;
+#endif
   for (int m = 0; m < 2 * kRadMaxNN; ++m) {
     double sd = 1.0;
     for (int a = 1; a <= m; ++a) sd *= std::sqrt((2.0 * a - 1) / (2.0 * a));
@@ -1430,6 +1506,7 @@ static void launch_rad(const RadArgs& a, bool radiances, hipStream_t st) {
 
 hipError_t launch_rad_chunk(int nn, const RadArgs& a, bool radiances, hipStream_t stream) {
   switch (nn) {
+#ifndef HD_RAD_WIDE
     case 1: launch_rad<1>(a, radiances, stream); break;
     case 2: launch_rad<2>(a, radiances, stream); break;
     case 3: launch_rad<3>(a, radiances, stream); break;
@@ -1438,15 +1515,31 @@ hipError_t launch_rad_chunk(int nn, const RadArgs& a, bool radiances, hipStream_
     case 6: launch_rad<6>(a, radiances, stream); break;
     case 7: launch_rad<7>(a, radiances, stream); break;
     case 8: launch_rad<8>(a, radiances, stream); break;
+    default: return wide::launch_rad_chunk(nn, a, radiances, stream);
+#else
+    case 9: launch_rad<9>(a, radiances, stream); break;
+    case 10: launch_rad<10>(a, radiances, stream); break;
+    case 11: launch_rad<11>(a, radiances, stream); break;
+    case 12: launch_rad<12>(a, radiances, stream); break;
+    case 13: launch_rad<13>(a, radiances, stream); break;
+    case 14: launch_rad<14>(a, radiances, stream); break;
+    case 15: launch_rad<15>(a, radiances, stream); break;
+    case 16: launch_rad<16>(a, radiances, stream); break;
     default: return hipErrorInvalidValue;
+#endif
   }
   return hipGetLastError();
 }
 
+#ifndef HD_RAD_WIDE
 size_t rad_scratch_doubles_per_unit(int nn, int nlyr) {
-  const size_t ne1r = (size_t)(nn * (nn + 1) + 2 * nn + 1);
+  const size_t ne1r = (size_t)rad_layer_record_doubles(nn);
   return (size_t)nlyr * (ne1r + rad_rec_doubles(nn) + rad_bsub_doubles(nn) + 4 * nn) +
          (size_t)2 * nn;
 }
+#endif
 
+#ifdef HD_RAD_WIDE
+}  // namespace wide
+#endif
 }  // namespace hd

@@ -1,6 +1,6 @@
 // hd_rad.hpp -- argument block and launchers of the intensity path
 // (hd_rad.hip): every azimuthal mode, user optical depths and user angles,
-// nstr <= 16 (one lane per (solve, mode) problem).
+// nstr <= 32 (one lane per (solve, mode) problem).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -9,11 +9,16 @@
 
 namespace hd {
 
-constexpr int kRadMaxNN = kMaxRegNN;
+constexpr int kRadMaxNN = kMaxNN;  // nstr <= 32 (NN > 8: rolled loops, private memory)
 
 template <int NN>
 __host__ __device__ constexpr int rad_nsym() {
   return NN * (NN + 1) / 2;
+}
+// per-(unit, layer) layer-operator record of the intensity kernels: the register
+// path's layout (R~, T~ upper, S~+, S~-, tau') at every nstr
+__host__ __device__ constexpr int rad_layer_record_doubles(int nn) {
+  return nn * (nn + 1) + 2 * nn + 1;
 }
 // per-(unit, layer) radiance record: L (packed lower), V, k, Z+, Z-, h, B_top,
 // dB/dtau', tau', omega', exp(-k tau'), exp(-tau'/mu0)
@@ -71,5 +76,10 @@ hipError_t upload_rad_tables(const QuadHost* per_nn);  // nn 1..kRadMaxNN
 // radiances = false: fluxes at the user depths only (mode 0, no uu)
 hipError_t launch_rad_chunk(int nn, const RadArgs& a, bool radiances, hipStream_t stream);
 size_t rad_scratch_doubles_per_unit(int nn, int nlyr);
+// nstr 18..32: the same kernels compiled with rolled NN-loops (hd_rad_wide.hip)
+namespace wide {
+hipError_t upload_rad_tables(const QuadHost* per_nn);
+hipError_t launch_rad_chunk(int nn, const RadArgs& a, bool radiances, hipStream_t stream);
+}  // namespace wide
 
 }  // namespace hd

@@ -21,7 +21,7 @@ also computes radiances -- at ``user_mu`` x ``user_phi`` with ``usrang``, else a
 the quadrature cosines and ``user_phi`` (default [0]) -- at ``user_tau`` with
 ``usrtau`` (else at the level depths); ``get_rad()`` returns them as
 (nwave, ncol, nphi, ntau, numu).  With ``usrtau`` the fluxes are at the user
-depths, (nwave, ncol, ntau, 2), index 0 = the deepest.  nstr <= 16 there.
+depths, (nwave, ncol, ntau, 2), index 0 = the deepest.  Every nstr 2..32.
 
 The arithmetic runs in libhdisort.so (HIP, gfx950) through the C-ABI in
 include/hdisort.h.  There is no CPU fallback: without a HIP device or without
@@ -158,9 +158,6 @@ class Disort(RTSolver):
         self.corint = bool(flags & {"intensity_correction", "old_intensity_correction"})
         self._rad = None
         if self.radiance:
-            if ds.nstr > 16:
-                raise RuntimeError(f"Disort: nstr={ds.nstr}; radiances / user depths need "
-                                   "nstr <= 16")
             if self.usrtau:
                 ut = [float(x) for x in op.user_tau()]
                 if not ut:

@@ -105,9 +105,11 @@ def _random_case(rng, nwave, ncol, nlyr, nstr, planck, rayleigh=False):
     return prop, bc, kw
 
 
-@pytest.mark.parametrize("nstr", [2, 4, 6, 8, 12, 16])
+@pytest.mark.parametrize("nstr", [2, 4, 6, 8, 12, 16, 18, 24, 32])
 @pytest.mark.parametrize("planck", [False, True])
 def test_radiances_vs_oracle(nstr, planck):
+    """Every azimuthal mode, user depths and angles; nstr 18..32 run the same
+    kernels compiled with rolled loops (hd_rad_wide.hip)."""
     rng = np.random.default_rng(500 + nstr + 50 * planck)
     nwave, ncol, nlyr = 2, 3, 6
     prop, bc, kw = _random_case(rng, nwave, ncol, nlyr, nstr, planck)
@@ -220,7 +222,7 @@ def test_radiance_chunking_invariance():
 
 def test_radiance_argument_errors():
     with pytest.raises(RuntimeError):
-        _disort(18, 2, 1, 1, flags="usrang,lamber", umu=[0.5], phi=[0.0])
+        _disort(34, 2, 1, 1, flags="usrang,lamber", umu=[0.5], phi=[0.0])
     with pytest.raises(RuntimeError):
         _disort(8, 2, 1, 1, flags="usrang,lamber", umu=[0.0], phi=[0.0])
     with pytest.raises(RuntimeError):
@@ -252,7 +254,7 @@ def test_cpp_disort_rad():
     assert abs(flux[0][1] - dn_bot) <= 5e-6 * dn_bot
 
 
-@pytest.mark.parametrize("nstr", [8, 16])
+@pytest.mark.parametrize("nstr", [8, 16, 24])
 def test_tms_corrected_radiances_vs_oracle(nstr):
     """intensity_correction on forward-peaked HG layers with 48 moments (delta-M
     truncation active): the TMS-corrected radiances vs the oracle's"""
