@@ -112,12 +112,21 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
   __shared__ double psi_lds[kPsi * kLayerBlock];  // Psi^T staged per lane
   const Quad<NN>& Qc = quad<NN>();
   // block = 64 consecutive solves (one wave each) x kLayersPerBlock consecutive
-  // layers: a wave's stores are coalesced (same layer, consecutive solves) and
-  // the block's waves read neighbouring records of the same solves (shared lines)
+  // layers: a wave's stores are coalesced (same layer, consecutive solves).
+  // Neighbouring layers of a solve share 128-B lines of prop (18 doubles per
+  // record), so the blocks of one solve tile are numbered layer-fastest and
+  // dealt to the same XCD (blocks b and b + 8 share an XCD's L2): the second
+  // reader of a line finds it in L2 instead of HBM
   const int lt = threadIdx.x;
-  const int ntile_s = (A.nsc + 63) / 64;
-  const int ts = blockIdx.x % ntile_s;
-  const int tl = blockIdx.x / ntile_s;
+  const int ntl = (A.nlyr + kLayersPerBlock - 1) / kLayersPerBlock;
+  int ts, tl;
+  {
+    const int nb = (int)gridDim.x, b = (int)blockIdx.x;
+    const int x = b & 7, base = nb >> 3, extra = nb & 7;
+    const int logical = x * base + (x < extra ? x : extra) + (b >> 3);
+    ts = logical / ntl;
+    tl = logical - ts * ntl;
+  }
   const int sl = ts * 64 + (lt & 63);
   const int lc = tl * kLayersPerBlock + (lt >> 6);  // solver layer, 0 = top
   const int L = A.nlyr;

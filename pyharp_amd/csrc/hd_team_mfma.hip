@@ -121,6 +121,16 @@ __device__ __forceinline__ void pin(double (&x)[NN]) {
 }
 __device__ __forceinline__ void pin(double& x) { asm volatile("" : "+v"(x)); }
 
+// XCD-aware block numbering (hardware deals blocks round-robin over the 8 XCDs):
+// the blocks of one XCD take consecutive logical ids, ordered layer-fastest
+__device__ __forceinline__ int block_logical() {
+  const int nb = (int)gridDim.x, b = (int)blockIdx.x;
+  const int x = b & 7, base = nb >> 3, extra = nb & 7;
+  return x * base + (x < extra ? x : extra) + (b >> 3);
+}
+__device__ __forceinline__ int block_group(int L) { return block_logical() / L; }
+__device__ __forceinline__ int block_layer(int L) { return block_logical() % L; }
+
 // lane i of each team: column i of the inverse of the lower-triangular J whose
 // rows the team holds (forward substitution J z = e_i), i.e. row i of J^-T
 template <int NN>
@@ -164,15 +174,16 @@ __global__ __launch_bounds__(64, 2) void hd_team_mfma_layer_kernel(LayerArgs A) 
   const bool act = i < NN;
   const int ii = act ? i : 0;
   const int L = A.nlyr;
-  const long total = (long)A.nsc * L;
-  long team = (long)blockIdx.x * 4 + t;
+  // block = 4 consecutive solves (one per team) of one layer: their records are
+  // contiguous.  Blocks are numbered layer-fastest within a group of solves and
+  // dealt to one XCD (blocks b and b + 8 share an L2), so the neighbouring
+  // layers of a solve -- which share prop's cache lines -- are read close together
+  const int grp = block_group(L);  // first solve of this block / 4
+  const int lc = block_layer(L);
   // every lane takes part in the MFMA and LDS exchanges: a team past the end
-  // recomputes the last item and stores nothing
-  const bool valid = team < total;
-  if (!valid) team = total - 1;
-  // consecutive teams = consecutive solves of one layer -> contiguous records
-  const int sl = (int)(team % A.nsc);
-  const int lc = (int)(team / A.nsc);
+  // recomputes the block's first solve and stores nothing
+  const bool valid = grp * 4 + t < A.nsc;
+  const int sl = valid ? grp * 4 + t : grp * 4;
   const long s = A.s0 + sl;
   const int nm = A.nmom;
   const int np = A.nprop;
@@ -423,10 +434,8 @@ __global__ __launch_bounds__(64, 2) void hd_team_mfma_layer_kernel(LayerArgs A) 
 #pragma unroll
   for (int tt = 0; tt < 4; ++tt) {
     double chk = 0.0;
-    long tm = (long)blockIdx.x * 4 + tt;
-    const bool ok = tm < total;
-    if (!ok) tm = total - 1;
-    const int slt = (int)(tm % A.nsc), lct = (int)(tm / A.nsc);
+    const bool ok = grp * 4 + tt < A.nsc;
+    const int slt = ok ? grp * 4 + tt : grp * 4, lct = lc;
     double* rec = A.scr + ((size_t)lct * A.nsc + slt) * ne1t<NN>();
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
@@ -468,8 +477,7 @@ hipError_t upload_quad_tables_team_mfma(const QuadTablesTeam& t) {
 
 template <int NN>
 static hipError_t launch_layer(const LayerArgs& la, hipStream_t stream) {
-  const long nt1 = (long)la.nsc * la.nlyr;
-  const unsigned nb1 = (unsigned)((nt1 + 3) / 4);
+  const unsigned nb1 = (unsigned)(((la.nsc + 3) / 4) * (long)la.nlyr);
   hipLaunchKernelGGL(hd_team_mfma_layer_kernel<NN>, dim3(nb1), dim3(64), 0, stream, la);
   return hipGetLastError();
 }

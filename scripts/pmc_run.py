@@ -12,7 +12,12 @@ prop, bc, _ = bench.make_inputs(list(range(W)), C, L, nstr, False, dev, **kw)
 op = DisortOptions().flags('lamber,quiet,onlyfl').nwave(W).ncol(C)
 op.ds().nlyr, op.ds().nstr, op.ds().nmom = L, nstr, nstr
 d = Disort(op)
+# the bench's path: the band sum fused into the solve (PMC_UNFUSED=1: hd_solve)
+wts = torch.full((W,), 1.0 / W, dtype=torch.float64, device=dev)
 for _ in range(2):
-    out = d.forward(prop, bc)
+    if os.environ.get("PMC_UNFUSED") == "1":
+        out = d.forward(prop, bc)
+    else:
+        out = d.forward_band(prop, bc, weights=wts)
 torch.cuda.synchronize()
-print('done', float(out[0, 0, -1, 0]))
+print('done', float(out.flatten()[-1]))
