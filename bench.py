@@ -401,10 +401,13 @@ def main():
         ach = k1_flop * solves_per_launch / (k1_avg_ms * 1e-3) / 1e12
         pmc = load_pmc(nstr, nlyr, args.planck)
         traffic = None
+        path_bytes = None
         if pmc:
             k1 = pmc["kernels"].get(f"{layer_kernel}<{nstr // 2}>")
             if k1:
                 traffic = round(k1["bytes_per_solve"] * solves_per_launch)
+            # HBM bytes per solve of every kernel of the path (one chunk's launches)
+            path_bytes = round(sum(k["bytes_per_solve"] for k in pmc["kernels"].values()))
         roofline = {"bound": "fp64-mfma+valu" if mfma else "fp64-valu", "kernel": f"{layer_kernel}<{nstr // 2}>", "achieved": round(ach, 3),
                     "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(ach / FP64_PEAK_TFLOPS, 4),
@@ -414,6 +417,9 @@ def main():
                     "(2 x FETCH_SIZE + WRITE_SIZE, scaled to this launch's solves); "
                     "algorithmic bytes per solve are much smaller: the layer records "
                     "(89 doubles per layer) are written to HBM scratch for the sweep",
+                    "path_bytes_per_solve": path_bytes,
+                    "algorithmic_bytes_per_solve": int(nlyr * (2 + nstr) * 8 + 48 + (nlyr + 1) * 16
+                                                       + (nlyr + 1) * 8 * int(bool(args.planck))),
                     "avg_launch_ms": round(k1_avg_ms, 3),
                     "flop_per_solve": k1_flop,
                     "note": ("FP64 compute bound: dense 16x16 products on FP64 MFMA, the "
