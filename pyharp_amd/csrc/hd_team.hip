@@ -583,6 +583,16 @@ static bool team_layer_valu() {
   return v;
 }
 
+// HD_TEAM_SWEEP=valu selects the VALU-product sweep (A/B runs); the default is
+// the MFMA one (hd_team_mfma.hip)
+static bool team_sweep_valu() {
+  static const bool v = [] {
+    const char* e = std::getenv("HD_TEAM_SWEEP");
+    return e && std::strcmp(e, "valu") == 0;
+  }();
+  return v;
+}
+
 template <int NN>
 static hipError_t launch_team(const PlanckArgs* pa, const TaucArgs* ta, const LayerArgs& la,
                               const SweepArgs& sa, hipStream_t stream, hipEvent_t* ev) {
@@ -601,6 +611,11 @@ static hipError_t launch_team(const PlanckArgs* pa, const TaucArgs* ta, const La
   }
   if (ev) (void)hipEventRecord(ev[1], stream);
   if (ev) (void)hipEventRecord(ev[2], stream);
+  if (!team_sweep_valu()) {
+    const hipError_t e = launch_team_sweep_mfma(NN, sa, stream);
+    if (ev) (void)hipEventRecord(ev[3], stream);
+    return e;
+  }
   hipLaunchKernelGGL(hd_team_sweep_kernel<NN>, dim3(nb2), dim3(kTeamBlock), 0, stream, sa);
   if (ev) (void)hipEventRecord(ev[3], stream);
   return hipGetLastError();
@@ -620,6 +635,7 @@ static hipError_t launch_team_layer(const LayerArgs& la, hipStream_t stream) {
 }
 template <int NN>
 static hipError_t launch_team_sweep(const SweepArgs& sa, hipStream_t stream) {
+  if (!team_sweep_valu()) return launch_team_sweep_mfma(NN, sa, stream);
   const unsigned nb2 = (unsigned)((sa.nsc + kTeamsPerBlock - 1) / kTeamsPerBlock);
   hipLaunchKernelGGL(hd_team_sweep_kernel<NN>, dim3(nb2), dim3(kTeamBlock), 0, stream, sa);
   return hipGetLastError();

@@ -471,6 +471,250 @@ __global__ __launch_bounds__(64, 2) void hd_team_mfma_layer_kernel(LayerArgs A) 
   }
 }
 
+// ============================================================================
+// K2 (team, MFMA): adding sweep + back-substitution, four solves per wave.
+// The register/team sweep's update per layer
+//   W1 = I - R A,  ZT = W1^-1 T,  A <- R + T A ZT,  Sd <- T (A t1 + Sd) + S-
+// (A = reflection of the stack above, t1 = W1^-1 (R Sd + S+)) with the three
+// dense 16 x 16 products (R A, A ZT, T (A ZT)) on the matrix core in the M
+// layout -- R~, T~ and A are symmetric, so each is its own transpose operand --
+// and the pivot-free LU of W1, the ZT solves and the vectors on the VALU in the
+// team layout (lane i = row i), as hd_team_sweep_kernel; W1 goes M -> T and ZT
+// T -> M through LDS, A is kept in both layouts.  Identical record formats, so
+// the back-substitution pass is hd_team_sweep_kernel's.  One wave per SIMD: at
+// two (256 registers) it spills 144 VGPRs and ran C5 at 0.81M solves/s against
+// 1.02M here and 0.97M for the VALU sweep (scripts/ab/sw_ab.sh).
+// ============================================================================
+template <int NN>
+__global__ __launch_bounds__(64, 1) void hd_team_mfma_sweep_kernel(SweepArgs A) {
+  __shared__ double lds[2 * kSet];
+  double* S0 = lds;
+  double* S1 = lds + kSet;
+  const Quad<NN>& Qc = tquad<NN>(c_qt);
+  const int lane = (int)threadIdx.x;
+  const int h = lane >> 4, c = lane & 15;  // M layout
+  const int t = h, i = c;                  // T layout: team t, row i
+  const bool act = i < NN;
+  const int ii = act ? i : 0;
+  const int grp = (int)blockIdx.x;
+  // every lane takes part in the MFMA / LDS / DPP exchanges: a team past the end
+  // repeats the block's first solve and stores nothing
+  const bool valid = grp * 4 + t < A.nsc;
+  const int sl = valid ? grp * 4 + t : grp * 4;
+  const long s = solve_of(A.s0 + sl, A.cmaj, A.nwave, A.ncol);
+  const int L = A.nlyr;
+  const size_t nsc = A.nsc;
+  int st = 0;
+  const double msk = act ? 1.0 : 0.0;
+  const double g_i = Qc.g[ii] * msk;
+
+  for (int k = lane; k < 2 * kSet; k += 64) lds[k] = 0.0;
+  lds_fence();
+
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
+  const double fb = A.fbeam ? A.fbeam[s] : 0.0;
+  const bool beam = fb > 0.0 && mu0 > 0.0;
+  const double alb = A.albedo ? A.albedo[s] : 0.0;
+  if (!(alb >= 0.0) || !(alb <= 1.0)) st |= kStBadInput;
+  double top = A.fisot ? A.fisot[s] : 0.0;
+  double bsurf = 0.0;
+  if (A.planck) {
+    bsurf = A.planckv[(size_t)(L + 1) * nsc + sl];
+    top += A.planckv[(size_t)(L + 2) * nsc + sl];
+  }
+  const double twopi = 2.0 * kPi;
+  const double rmu0 = beam ? 1.0 / mu0 : 0.0;
+  const double f0mu0 = beam ? fb * mu0 : 0.0;
+
+  // the wave's four solves in M layout: problem tt's records
+  int slm[4];
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt) slm[tt] = grp * 4 + tt < A.nsc ? grp * 4 + tt : grp * 4;
+
+  double ram[4][4];  // A (M layout)
+  double ra[NN];     // A row i (T layout)
+  double sd = g_i * top;
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) ram[tt][m] = 0.0;
+  sfor<0, NN>([&](auto J) { ra[HD_K(J)] = 0.0; });
+  double tauc = 0.0;
+
+  for (int lc = 0; lc < L; ++lc) {
+    const double* rec = A.scr + ((size_t)lc * nsc + sl) * ne1t<NN>();
+    double* bp = A.bsub + ((size_t)lc * nsc + sl) * ne2t<NN>();
+    double* bw = (act && valid) ? bp : A.sink;
+    // R~, T~ of the four problems in M layout (zero padding beyond NN)
+    double rm[4][4], tm[4][4];
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      const double* rt = A.scr + ((size_t)lc * nsc + slm[tt]) * ne1t<NN>();
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int r = h + 4 * m;
+        const bool in = r < NN && c < NN;
+        const int e = in ? r * NN + c : 0;
+        rm[tt][m] = in ? rt[e] : 0.0;
+        tm[tt][m] = in ? rt[NN * NN + e] : 0.0;
+      }
+    }
+    // this problem's rows in T layout
+    double rl[NN], tr[NN];
+    sfor<0, NN>([&](auto J) {
+      rl[HD_K(J)] = rec[ii * NN + HD_K(J)] * msk;
+      tr[HD_K(J)] = rec[NN * NN + ii * NN + HD_K(J)] * msk;
+    });
+    const double spl = rec[2 * NN * NN + ii] * msk;
+    const double sml = rec[2 * NN * NN + NN + ii] * msk;
+
+    // level lc (top of layer lc): F_dn = rc . I+ + cs
+    {
+      double tq = 0.0;
+      sfor<0, NN>([&](auto J) { tq = fma(ra[HD_K(J)], Qc.g[HD_K(J)], tq); });
+      bw[NN * NN + NN + ii] = twopi * tq;
+      const double cs = team_sum(g_i * sd);
+      if (i == 0 && valid) bp[NN * NN + 2 * NN] = fma(twopi, cs, f0mu0 * exp(-tauc * rmu0));
+    }
+    // W1 = I - R A on the matrix core, to team rows through LDS
+    {
+      double pw[4][4];
+      mprod<false>(rm, ram, pw, h, c);
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) pw[tt][m] = (h + 4 * m == c ? 1.0 : 0.0) - pw[tt][m];
+      lds_fence();
+      put_m(S0, h, c, pw);
+      lds_fence();
+    }
+    double w[NN];
+    get_rows<NN>(S0, t, i, w);
+    sfor<0, NN>([&](auto J) { w[HD_K(J)] *= msk; });
+    // t1 = R Sd + S+
+    double t1 = spl;
+    sfor<0, NN>([&](auto K) { t1 = fma(rl[HD_K(K)], bc<HD_K(K)>(sd), t1); });
+    // LU without pivoting; reciprocal pivots on the diagonal
+    sfor<0, NN>([&](auto K) {
+      constexpr int k = HD_K(K);
+      const double piv = bc<k>(w[k]);
+      if (!(fabs(piv) > 1.0e-12)) st |= kStPivot;
+      const double rp = rcp_nr(piv);
+      const double lik = w[k] * rp;
+      const double mm = i > k ? lik : 0.0;
+      w[k] = i == k ? rp : (i > k ? lik : w[k]);
+      sfor<k + 1, NN>([&](auto J) {
+        constexpr int j = HD_K(J);
+        w[j] = fma(-mm, bc<k>(w[j]), w[j]);
+      });
+    });
+    // t1 <- W1^-1 t1
+    sfor<0, NN>([&](auto K) {
+      constexpr int k = HD_K(K);
+      const double tk = bc<k>(t1);
+      if (i > k) t1 = fma(-w[k], tk, t1);
+    });
+    sfor_rev<0, NN>([&](auto K) {
+      constexpr int k = HD_K(K);
+      if (i == k) t1 *= w[k];
+      const double tk = bc<k>(t1);
+      if (i < k) t1 = fma(-w[k], tk, t1);
+    });
+    // u = A t1 + Sd
+    double u = sd;
+    sfor<0, NN>([&](auto K) { u = fma(ra[HD_K(K)], bc<HD_K(K)>(t1), u); });
+    bw[NN * NN + ii] = t1;
+    // ZT = W1^-1 T (row-sequential solves) -> record, and to M layout through LDS
+    double zt[NN];
+    sfor<0, NN>([&](auto J) { zt[HD_K(J)] = tr[HD_K(J)]; });
+    sfor<0, NN>([&](auto K) {
+      constexpr int k = HD_K(K);
+      const double mm = i > k ? w[k] : 0.0;
+      sfor<0, NN>([&](auto J) { zt[HD_K(J)] = fma(-mm, bc<k>(zt[HD_K(J)]), zt[HD_K(J)]); });
+    });
+    sfor_rev<0, NN>([&](auto K) {
+      constexpr int k = HD_K(K);
+      const double sc = i == k ? w[k] : 1.0;
+      sfor<0, NN>([&](auto J) { zt[HD_K(J)] *= sc; });
+      const double mm = i < k ? w[k] : 0.0;
+      sfor<0, NN>([&](auto J) { zt[HD_K(J)] = fma(-mm, bc<k>(zt[HD_K(J)]), zt[HD_K(J)]); });
+    });
+    sfor<0, NN>([&](auto J) { bw[ii * NN + HD_K(J)] = zt[HD_K(J)]; });
+    sfor<0, NN>([&](auto J) { zt[HD_K(J)] *= msk; });
+    put_rows<NN>(S1, t, i, zt);
+    // Sd <- T u + S-
+    {
+      double tq = sml;
+      sfor<0, NN>([&](auto K) { tq = fma(tr[HD_K(K)], bc<HD_K(K)>(u), tq); });
+      sd = tq * msk;
+    }
+    lds_fence();
+    // A <- R + T (A ZT) on the matrix core; then A's rows to the team layout
+    {
+      double zm[4][4], pm[4][4];
+      get_m(S1, h, c, zm);
+      mprod<false>(ram, zm, pm, h, c);  // A ZT   (A symmetric: its own transpose)
+      mprod<false>(tm, pm, ram, h, c);  // T (A ZT)
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) ram[tt][m] += rm[tt][m];
+      lds_fence();
+      put_m(S0, h, c, ram);
+      lds_fence();
+    }
+    get_rows<NN>(S0, t, i, ra);
+    sfor<0, NN>([&](auto J) { ra[HD_K(J)] *= msk; });
+    tauc += rec[2 * NN * NN + 2 * NN];
+  }
+
+  // ---- Lambertian surface: I+ = g x ----
+  double rgrow = 0.0;
+  sfor<0, NN>([&](auto J) { rgrow = fma(ra[HD_K(J)], Qc.g[HD_K(J)], rgrow); });
+  const double gsd = bc<0>(team_sum(g_i * sd));
+  const double grg = bc<0>(team_sum(g_i * rgrow));
+  double esurf = (1.0 - alb) * bsurf;
+  const double dirsurf = f0mu0 * exp(-tauc * rmu0);
+  if (beam) esurf += alb * dirsurf / kPi;
+  const double x = (2.0 * alb * gsd + esurf) / (1.0 - 2.0 * alb * grg);
+  double ip = g_i * x;
+  double* fo = A.flux + (size_t)(A.flux_local ? (long)sl : s) * (L + 1) * 2;
+  double chk = 0.0;
+  {
+    const double up = team_sum(g_i * ip);
+    const double dn = team_sum(g_i * fma(rgrow, x, sd));
+    if (i == 0 && valid) {
+      fo[0] = twopi * up;
+      fo[1] = twopi * dn + dirsurf;
+    }
+    chk += twopi * up + twopi * dn;
+  }
+  // ---- back-substitution bottom -> top ----
+  for (int lc = L - 1; lc >= 0; --lc) {
+    const double* bp = A.bsub + ((size_t)lc * nsc + sl) * ne2t<NN>();
+    double nip = bp[NN * NN + ii] * msk;
+    sfor<0, NN>([&](auto J) {
+      const double z = bp[ii * NN + HD_K(J)] * msk;
+      nip = fma(z, bc<HD_K(J)>(ip), nip);
+    });
+    const double rc = bp[NN * NN + NN + ii] * msk;
+    const double up = team_sum(g_i * nip);
+    const double dn = team_sum(rc * nip);
+    ip = nip;
+    if (i == 0 && valid) {
+      const int lev = L - lc;
+      fo[2 * lev] = twopi * up;
+      fo[2 * lev + 1] = bp[NN * NN + 2 * NN] + dn;
+    }
+    chk += twopi * up + dn;
+  }
+  if (!isfinite(chk)) st |= kStNonFinite;
+  if (valid && st) {
+    atomicOr(&A.status[s], st);
+    if (st & 0x0F) atomicOr(A.anyerr, 1);
+  }
+}
+
 hipError_t upload_quad_tables_team_mfma(const QuadTablesTeam& t) {
   return hipMemcpyToSymbol(HIP_SYMBOL(c_qt), &t, sizeof(t), 0, hipMemcpyHostToDevice);
 }
@@ -480,6 +724,27 @@ static hipError_t launch_layer(const LayerArgs& la, hipStream_t stream) {
   const unsigned nb1 = (unsigned)(((la.nsc + 3) / 4) * (long)la.nlyr);
   hipLaunchKernelGGL(hd_team_mfma_layer_kernel<NN>, dim3(nb1), dim3(64), 0, stream, la);
   return hipGetLastError();
+}
+
+template <int NN>
+static hipError_t launch_sweep(const SweepArgs& sa, hipStream_t stream) {
+  hipLaunchKernelGGL(hd_team_mfma_sweep_kernel<NN>, dim3((unsigned)((sa.nsc + 3) / 4)), dim3(64),
+                     0, stream, sa);
+  return hipGetLastError();
+}
+
+hipError_t launch_team_sweep_mfma(int nn, const SweepArgs& sa, hipStream_t stream) {
+  switch (nn) {
+    case 9: return launch_sweep<9>(sa, stream);
+    case 10: return launch_sweep<10>(sa, stream);
+    case 11: return launch_sweep<11>(sa, stream);
+    case 12: return launch_sweep<12>(sa, stream);
+    case 13: return launch_sweep<13>(sa, stream);
+    case 14: return launch_sweep<14>(sa, stream);
+    case 15: return launch_sweep<15>(sa, stream);
+    case 16: return launch_sweep<16>(sa, stream);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_team_layer_mfma(int nn, const LayerArgs& la, hipStream_t stream) {
