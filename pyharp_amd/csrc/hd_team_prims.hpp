@@ -225,9 +225,19 @@ constexpr double kJacobiTol2 = 1.0e-30;  // rotate while (b_p.b_q)^2 > tol |b_p|
 // bound for the same residual, ~4e-15)
 constexpr double kJacobiLastFrob2 = 1.0e-16;
 
+// Column scales (HD_JACOBI_SCALED): lane j holds b_j = sig_j x_j, so a rotation
+//   b_p' = c b_p - s b_q  becomes  x_p' = x_p - (s sig_q / (c sig_p)) x_q,  sig_p' = c sig_p
+// -- one FMA per element instead of a MUL and an FMA (c >= 1/sqrt(2), so the
+// scales shrink by at most 2^-1/2 per rotation; they are folded back into x at
+// every sweep start).  The rotation angle, the tracked norms and the stop rule
+// are those of the unscaled form.
+#ifndef HD_JACOBI_SCALED
+#define HD_JACOBI_SCALED 1
+#endif
+
 template <int NN, int M>
-__device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double& own, bool on,
-                                                  double& off) {
+__device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double& own, double& sig,
+                                                  bool on, double& off) {
   const int i = tlane();
   const int pi = i ^ M;
   double bq[NN];
@@ -239,7 +249,12 @@ __device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double& own, 
     if constexpr (k % 2 == 0) g0 = fma(b[k], bq[k], g0);
     else g1 = fma(b[k], bq[k], g1);
   });
+#if HD_JACOBI_SCALED
+  const double sq = xswz<M>(sig);
+  const double gam = (g0 + g1) * (sig * sq);
+#else
   const double gam = g0 + g1;
+#endif
   const bool lo = i < pi;
   const double app = lo ? own : oth;
   const double aqq = lo ? oth : own;
@@ -257,7 +272,14 @@ __device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double& own, 
   const double c = r ? u * z : 1.0;
   const double s = r ? sg * gam * z : 0.0;
   const double se = lo ? -s : s;  // p side: c b_p - s b_q ; q side: s b_p + c b_q
+#if HD_JACOBI_SCALED
+  const double tq = se * sq * rcp_nr(c * sig);
+  sfor<0, NN>([&](auto K) { b[HD_K(K)] = fma(tq, bq[HD_K(K)], b[HD_K(K)]); });
+  sig *= c;
+#else
+  (void)sig;
   sfor<0, NN>([&](auto K) { b[HD_K(K)] = fma(se, bq[HD_K(K)], c * b[HD_K(K)]); });
+#endif
   // rotated norms: |c b_p - s b_q|^2 and |s b_p + c b_q|^2
   const double cc = c * c, ss2 = s * s, cs2 = 2.0 * c * s * gam;
   own = lo ? fma(cc, app, fma(ss2, aqq, -cs2)) : fma(ss2, app, fma(cc, aqq, cs2));
@@ -269,19 +291,25 @@ __device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double& own, 
 template <int NN>
 __device__ __forceinline__ void team_jacobi(double (&b)[NN], int max_sweeps) {
   bool on = true;
+  double sig = 1.0;  // b = sig x (HD_JACOBI_SCALED)
   for (int sweep = 0; sweep < max_sweeps; ++sweep) {
     double off = 0.0;  // this lane's sum of (b_p.b_q)^2 over its pairs in this sweep
     double own = 0.0;  // |b_j|^2, exact at the start of every sweep, then tracked
-    sfor<0, NN>([&](auto K) { own = fma(b[HD_K(K)], b[HD_K(K)], own); });
+    sfor<0, NN>([&](auto K) {
+      b[HD_K(K)] *= sig;
+      own = fma(b[HD_K(K)], b[HD_K(K)], own);
+    });
+    sig = 1.0;
     const double dia = bc<0>(team_sum(own * own));  // sum_j |b_j|^4 (team-uniform)
     sfor<1, kTeam>([&](auto Mc) {
       constexpr int m = HD_K(Mc);
-      if constexpr (round_has_pair<NN>(m)) team_jacobi_round<NN, m>(b, own, on, off);
+      if constexpr (round_has_pair<NN>(m)) team_jacobi_round<NN, m>(b, own, sig, on, off);
     });
     // every pair was counted twice (once per lane): compare 2x the bound
     on = on && bc<0>(team_sum(off)) > 2.0 * kJacobiLastFrob2 * dia;
     if (__all(!on)) break;
   }
+  sfor<0, NN>([&](auto K) { b[HD_K(K)] *= sig; });
 }
 
 }  // namespace team
