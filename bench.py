@@ -275,7 +275,18 @@ def main():
     # ranks (ranks share devices, gloo instead of RCCL); never set by the driver
     rehearse = os.environ.get("HD_BENCH_REHEARSE") == "1"
     dev_index = local_rank % torch.cuda.device_count() if rehearse else local_rank
-    if world > 1:
+    # under torch.distributed.run the process group is set up even at one rank, so
+    # the RCCL initialisation and the band all-reduce run at every N
+    dist_on = world > 1 or "LOCAL_RANK" in os.environ
+    # RCCL prints a version banner on stdout when a communicator is created: send
+    # fd 1 to stderr until the warm-up's all-reduce is done, so stdout carries
+    # only the JSON line
+    saved_stdout = None
+    if dist_on:
+        sys.stdout.flush()
+        saved_stdout = os.dup(1)
+        os.dup2(2, 1)
+    if dist_on:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(dev_index)
@@ -290,7 +301,7 @@ def main():
     from pyharp_amd.disort import _context
 
     ncol, nlyr, nstr, G = args.ncol, args.nlyr, args.nstr, args.ngpoint
-    from pyharp_amd.spectral import allreduce_band_flux, band_flux, shard_gpoints
+    from pyharp_amd.spectral import band_flux, shard_gpoints
     gpoints = shard_gpoints(G, world, rank)
     W = len(gpoints)
     lw = cfgd.get("lw", False)
@@ -344,15 +355,22 @@ def main():
             graph.replay()
         else:
             solve()
-        return allreduce_band_flux(band)
+        if dist_on:
+            import torch.distributed as dist
+            dist.all_reduce(band, op=dist.ReduceOp.SUM)
+        return band
 
-    for _ in range(args.warmup):
+    for _ in range(max(args.warmup, 1 if dist_on else 0)):
         step()
     torch.cuda.synchronize()
+    if saved_stdout is not None:
+        sys.stdout.flush()
+        os.dup2(saved_stdout, 1)
+        os.close(saved_stdout)
     if int((status & 0xF).any()):
         raise RuntimeError("bench: solver reported errors in the warm-up")
     ctx = _context(dev_index)
-    if world > 1:
+    if dist_on:
         import torch.distributed as dist
         dist.barrier()
     torch.cuda.synchronize()
@@ -361,7 +379,7 @@ def main():
     for _ in range(args.steps):
         band = step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     tm = ctx.timing()
@@ -378,7 +396,7 @@ def main():
         timing_note = "HIP events on one eager step after the graph-replayed timed steps"
     else:
         steps_timed = args.steps
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -469,14 +487,14 @@ def main():
                                     "fluxes not stored)" if fuse else
                                     "per-g fluxes stored (hd_solve) + hd_band_flux"),
                        "collective": ("all_reduce of the g-weighted band flux (" +
-                                      ("gloo, rehearsal" if rehearse else "RCCL") + ")") if world > 1
+                                      ("gloo, rehearsal" if rehearse else "RCCL") + ")") if dist_on
                        else "none"},
             "roofline": roofline, "path_roofline": whole, "cpu_baseline": cpu,
             "max_rel_err_vs_cpu_restatement": max_err,
             "band_fused_vs_unfused_max_rel": fused_vs_unfused,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 
