@@ -165,15 +165,18 @@ int hd_solve_band(hd_context *ctx, const hd_config *cfg, const hd_inputs *in,
  *   phi    HOST [nphi] user azimuths [deg]
  *   phi0   DEVICE [nwave*ncol] beam azimuth [deg] or NULL (0)
  *   onlyfl 1: fluxes at the user depths only (uu untouched)
- *   corint 1: Nakajima-Tanaka TMS correction of the beam's single scattering
- *          (flag intensity_correction; DISORT 2.0 INTCOR, STWL eq. 68)
+ *   corint 1: Nakajima-Tanaka correction of the beam radiances (flags
+ *          intensity_correction / old_intensity_correction; DISORT 2.0 INTCOR):
+ *          TMS (exact single scattering, STWL eq. 68) plus, for downward
+ *          directions, minus the IMS secondary-scattering term (STWL A.13-A.16)
  * Outputs (device):
  *   flux [nwave][ncol][ntau][2]  index 0 = the deepest user depth (harp order,
  *        as the level fluxes of hd_solve), [..][0] up, [..][1] rfldir + rfldn
  *   uu   [nwave][ncol][nphi][ntau][numu]  radiance, user order
  *        (cdisort's uu[j][lu][iu] per solve)
- * The IMS secondary-scattering term and cdisort's new correction are not
- * applied (all corrections vanish where the truncation does, chi_nstr = 0).
+ * cdisort's new (Buras-Emde-Dowling) correction is not restated: either flag
+ * applies the old one (all corrections vanish where the truncation does,
+ * chi_nstr = 0).
  */
 typedef struct hd_radiance {
   int ntau;

@@ -31,13 +31,16 @@ c_fluxes        :func:`disort_rad_column` (fluxes at the user depths)
 azimuth sum     uu = sum_m uum cos(m (phi - phi0)), phi in degrees
 ==============  ===========================================================
 
-Intensity correction: :func:`tms_correction` restates the Nakajima-Tanaka TMS
-step of DISORT 2.0's INTCOR (exact single scattering with the full moment
-series in place of the delta-M one).  Not restated: the IMS secondary-scattering
-term of the old correction and cdisort's new (Buras-Emde-Dowling) correction.
-All of them vanish when the delta-M truncation does (f = chi_nstr = 0, e.g.
-isotropic or Rayleigh phase functions, the ``tests/test_disort.cpp``
-configuration).
+Intensity correction (the "old" Nakajima-Tanaka correction of DISORT 2.0's
+INTCOR, cdisort's ``old_intensity_correction``): :func:`tms_correction`, the TMS
+step (exact single scattering with the full moment series in place of the
+delta-M one, STWL eq. 68), and :func:`ims_correction`, the IMS step (secondary
+scattering through the truncated forward peak, STWL eqs. A.13-A.16; SECSCA /
+XIFUNC in DISORT 2.0, ``c_secondary_scat`` / ``c_xi_func`` in cdisort), which is
+subtracted from the downward radiances.  Not restated: cdisort's new
+(Buras-Emde-Dowling) correction.  All of them vanish when the delta-M
+truncation does (f = chi_nstr = 0, e.g. isotropic or Rayleigh phase
+functions, the ``tests/test_disort.cpp`` configuration).
 
 Parity status: **parity unpinned** against cdisort (absent).  Pinned by known
 answers in ``tests/test_rad_oracle.py``: quadrature-angle intensities equal the
@@ -131,8 +134,9 @@ def disort_rad_column(dtauc, ssalb, pmom, nstr, *, umu, phi, utau, umu0=1.0, phi
                       onlyfl=False, corint=False):
     """One DISORT solve with intensities (layers top->bottom, cdisort order).
 
-    corint: the Nakajima-Tanaka TMS correction of the beam's single scattering
-    (see :func:`tms_correction`).
+    corint: the Nakajima-Tanaka correction of the beam's single (TMS,
+    :func:`tms_correction`) and secondary (IMS, :func:`ims_correction`)
+    scattering.
 
     umu: user polar cosines (nonzero), phi: user azimuths [deg], utau: user
     optical depths (unscaled, ascending).  Returns dict with ``uu``
@@ -178,7 +182,8 @@ def disort_rad_column(dtauc, ssalb, pmom, nstr, *, umu, phi, utau, umu0=1.0, phi
     out["uu"] = np.einsum("mj,mtu->jtu", cosm, uum)
     if corint and beam and not onlyfl:
         out["uu"] = out["uu"] + tms_correction(dtauc, ssalb, pmom, nstr, umu, phi, lay, utaupr,
-                                               taucpr, umu0, phi0, fbeam)
+                                               taucpr, umu0, phi0, fbeam) \
+            - ims_correction(dtauc, ssalb, pmom, nstr, umu, phi, lay, utau, umu0, phi0, fbeam)
     out["uum"] = uum
     return out
 
@@ -389,6 +394,85 @@ def tms_correction(dtauc, ssalb, pmom, nstr, umu, phi, lay, utaupr, taucpr, umu0
             for t, (lc, tau) in enumerate(zip(lay, utaupr)):
                 out[j, t, iu] = _sinsca(phast, ssalb, taucpr, lc, tau, mu, umu0, fbeam) - \
                     _sinsca(phasm, oprim, taucpr, lc, tau, mu, umu0, fbeam)
+    return out
+
+
+IMS_TINY = 1.0e-4  # SECSCA's cut: no IMS term when omega-bar, f-bar, the depth or fbeam <= it
+
+
+def xi_func(mu1, mu2, tau):
+    """STWL eq. (A.16): the geometric factor of twice-scattered beam light that
+    stays in the forward peak.  The beam (cosine mu2) is scattered at depth t'
+    into the same direction, again at t >= t', then travels to tau in direction
+    mu1:  (1/(mu1 mu2)) int_0^tau e^{-(tau-t)/mu1} int_0^t e^{-(t-t')/mu2}
+    e^{-t'/mu2} dt' dt  = [e^{-tau/mu1} - e^{-tau/mu2}(1 + a tau)] / (a^2 mu1 mu2),
+    a = 1/mu2 - 1/mu1;  tau^2 e^{-tau/mu1} / (2 mu1 mu2) at a = 0.  Near a = 0
+    the bracket is summed as e^{-tau/mu1} x^2 h(x), x = a tau,
+    h(x) = sum_{k>=2} (-1)^k (k-1)/k! x^(k-2) (no cancellation)."""
+    if tau <= 0.0:
+        return 0.0
+    a = 1.0 / mu2 - 1.0 / mu1
+    x = a * tau
+    e1 = math.exp(-tau / mu1)
+    if abs(x) < 0.5:
+        h, term = 0.0, 1.0  # term = (-x)^(k-2), fact = k!
+        fact = 2.0
+        for k in range(2, 24):
+            h += (k - 1) / fact * term
+            term *= -x
+            fact *= k + 1
+        return e1 * tau * tau / (mu1 * mu2) * h
+    return (e1 - math.exp(-tau / mu2) * (1.0 + x)) / (a * a * mu1 * mu2)
+
+
+def ims_correction(dtauc, ssalb, pmom, nstr, umu, phi, lay, utau, umu0, phi0, fbeam):
+    """IMS step of the Nakajima-Tanaka correction (DISORT 2.0 INTCOR/SECSCA,
+    STWL eqs. A.13-A.16): the secondary scattering that the TMS step gets wrong
+    because delta-M treats the truncated forward peak as exactly forward.
+
+    Above the user depth (unscaled; layers full, the user's layer down to it)
+    the omega- and f-weighted averages omega-bar, f-bar (eq. A.15) describe a
+    homogeneous slab; the peak's normalised phase function P'' has moments 1
+    for l < nstr and g_l = <omega chi_l> / <omega f> for l >= nstr, and
+    2 P'' - P''*P'' (moments 2 g_l - g_l^2, Funk-Hecke) is the angular part.
+    Returns the (nphi, ntau, numu) term to SUBTRACT from the radiances; zero
+    for upward directions.
+
+        I_IMS = F0/(4 pi) (f w)^2 / (1 - f w) PSPIKE(cos Theta)
+                * xi(|mu|, mu0 / (1 - f w), tau)
+    """
+    ssalb = np.where(np.asarray(ssalb, np.float64) == 1.0, 1.0 - DITHER, ssalb)
+    dtauc = np.asarray(dtauc, np.float64)
+    nlyr = len(dtauc)
+    nmom = pmom.shape[1] - 1
+    f = pmom[:, nstr] if nmom >= nstr else np.zeros(nlyr)
+    tauc = np.concatenate([[0.0], np.cumsum(dtauc)])
+    out = np.zeros((len(phi), len(utau), len(umu)))
+    for t, (lc, u) in enumerate(zip(lay, utau)):
+        dt = np.zeros(nlyr)
+        dt[:lc] = dtauc[:lc]
+        dt[lc] = max(0.0, u - tauc[lc])
+        wt = ssalb * dt
+        wsum, fsum, stau = wt.sum(), (wt * f).sum(), dt.sum()
+        if wsum <= IMS_TINY or fsum <= IMS_TINY or stau <= IMS_TINY or fbeam <= IMS_TINY:
+            continue
+        gk = {k: (wt @ pmom[:, k]) / fsum for k in range(nstr, nmom + 1)}
+        fbar, wbar = fsum / wsum, wsum / stau
+        fw = fbar * wbar
+        mu0p = umu0 / (1.0 - fw)
+        for iu, mu in enumerate(umu):
+            if mu >= 0.0:
+                continue
+            xi = xi_func(-mu, mu0p, u)
+            for j, ph in enumerate(phi):
+                ct = -mu * umu0 + math.sqrt(max(0.0, 1 - mu * mu)) * \
+                    math.sqrt(max(0.0, 1 - umu0 * umu0)) * math.cos(math.radians(ph - phi0))
+                pl = legendre_table(nmom + 1, [ct])[:, 0]
+                ps = 0.0
+                for k in range(nmom + 1):
+                    wk = 1.0 if k < nstr else gk[k] * (2.0 - gk[k])
+                    ps += (2 * k + 1) * wk * pl[k]
+                out[j, t, iu] = fbeam / (4.0 * math.pi) * fw * fw / (1.0 - fw) * ps * xi
     return out
 
 

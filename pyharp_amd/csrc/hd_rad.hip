@@ -1316,9 +1316,86 @@ __global__ __launch_bounds__(256) void hd_rad_azimuth_kernel(RadArgs A) {
 
 
 // ============================================================================
-// Nakajima-Tanaka TMS correction (DISORT 2.0 INTCOR, STWL eq. 68): exact single
-// scattering (full moment series, omega/(1 - f omega)) minus the delta-M one
-// (truncated series, omega'), both on the scaled depths; added to uu
+// IMS step of the Nakajima-Tanaka correction (DISORT 2.0 SECSCA / XIFUNC, STWL
+// eqs. A.13-A.16), without the F0/(4 pi) factor: secondary scattering through
+// the truncated forward peak, which delta-M (and so the TMS step) treats as
+// exactly forward.  The slab above the user depth tu (unscaled; the user's
+// layer lu_l down to tu) is replaced by its omega- and f-weighted averages;
+// the peak's phase function P'' has moments 1 below nstr and
+// g_l = <omega chi_l>/<omega f> from nstr on, and PSPIKE = 2 P'' - P''*P''
+// (moments 2 g - g^2).  Same arithmetic as oracle/disort_rad_np.py's
+// ims_correction / xi_func.  mu1 = |mu| of a downward user direction.
+// ============================================================================
+__device__ double ims_term(const RadArgs& A, long s, int nstr, double ct, double mu1, double mu0,
+                           double tu, int lu_l) {
+  constexpr double kTiny = 1.0e-4;
+  const int L = A.nlyr, np = A.nprop, nm = A.nmom;
+  if (nm < nstr) return 0.0;  // no truncation: f = 0
+  const double* q0 = A.prop + (size_t)s * L * np;
+  // dtau of solver layer lc above tu (harp layer L-1-lc); ssalb dithered as in setdis
+  auto slab = [&](int lc, double& ssa) {
+    const double* q = q0 + (size_t)(L - 1 - lc) * np;
+    ssa = np > 1 ? q[1] : 0.0;
+    if (ssa == 1.0) ssa = 1.0 - kDither;
+    if (lc < lu_l) return q[0];
+    const double d = tu - A.taus[(size_t)lc * A.ns + (s - A.s0)];
+    return d > 0.0 ? d : 0.0;
+  };
+  double wsum = 0.0, fsum = 0.0, stau = 0.0;
+  for (int lc = 0; lc <= lu_l; ++lc) {
+    double ssa;
+    const double dt = slab(lc, ssa);
+    const double wt = ssa * dt;
+    wsum += wt;
+    fsum = fma(wt, q0[(size_t)(L - 1 - lc) * np + 1 + nstr], fsum);
+    stau += dt;
+  }
+  if (!(wsum > kTiny) || !(fsum > kTiny) || !(stau > kTiny)) return 0.0;
+  const double fw = fsum / stau;  // f-bar omega-bar
+  // PSPIKE by the Legendre recurrence at cos(Theta)
+  double ps = 1.0, p1 = 1.0, p2 = 0.0;
+  for (int k = 1; k <= nm; ++k) {
+    const double pk = ((2 * k - 1) * ct * p1 - (k - 1) * p2) / k;
+    p2 = p1;
+    p1 = pk;
+    double wk = 1.0;
+    if (k >= nstr) {
+      double gs = 0.0;
+      for (int lc = 0; lc <= lu_l; ++lc) {
+        double ssa;
+        const double dt = slab(lc, ssa);
+        gs = fma(ssa * dt, q0[(size_t)(L - 1 - lc) * np + 1 + k], gs);
+      }
+      const double g = gs / fsum;
+      wk = g * (2.0 - g);
+    }
+    ps = fma((2 * k + 1) * wk, pk, ps);
+  }
+  // xi(mu1, mu2, tu), mu2 = mu0 / (1 - f w)
+  const double mu2 = mu0 / (1.0 - fw);
+  const double a = 1.0 / mu2 - 1.0 / mu1;
+  const double x = a * tu;
+  const double e1 = exp(-tu / mu1);
+  double xi;
+  if (fabs(x) < 0.5) {
+    double h = 0.0, term = 1.0, fact = 2.0;  // sum_{k>=2} (-1)^k (k-1)/k! x^(k-2)
+    for (int k = 2; k < 24; ++k) {
+      h += (k - 1) / fact * term;
+      term *= -x;
+      fact *= k + 1;
+    }
+    xi = e1 * tu * tu / (mu1 * mu2) * h;
+  } else {
+    xi = (e1 - exp(-tu / mu2) * (1.0 + x)) / (a * a * mu1 * mu2);
+  }
+  return fw * fw / (1.0 - fw) * ps * xi;
+}
+
+// ============================================================================
+// Nakajima-Tanaka correction (DISORT 2.0 INTCOR): the TMS step (STWL eq. 68),
+// exact single scattering (full moment series, omega/(1 - f omega)) minus the
+// delta-M one (truncated series, omega'), both on the scaled depths, and for
+// downward directions minus the IMS term (ims_term); added to uu
 // ============================================================================
 __global__ __launch_bounds__(256) void hd_rad_tms_kernel(RadArgs A, int nstr) {
   const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1394,6 +1471,7 @@ __global__ __launch_bounds__(256) void hd_rad_tms_kernel(RadArgs A, int nstr) {
       acc = fma(w, seg, acc);
     }
   }
+  if (mu < 0.0 && fb > 1.0e-4) acc -= ims_term(A, s, nstr, ct, -mu, mu0, tu, lu_l);  // SECSCA: fbeam > tiny
   A.uu[(((size_t)s * A.nphi + j) * A.ntau + lu) * A.numu + iu] += fb / (4.0 * kPi) * acc;
 }
 

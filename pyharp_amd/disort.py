@@ -153,8 +153,8 @@ class Disort(RTSolver):
         self.usrtau = "usrtau" in flags
         self.usrang = "usrang" in flags
         self.radiance = (not self.onlyfl) or self.usrtau
-        # Nakajima-Tanaka TMS correction (either correction flag; the IMS term and
-        # cdisort's new method are not applied -- DESIGN.md section 8)
+        # Nakajima-Tanaka correction, TMS + IMS (either correction flag; cdisort's
+        # new method is not restated -- DESIGN.md section 8)
         self.corint = bool(flags & {"intensity_correction", "old_intensity_correction"})
         self._rad = None
         if self.radiance:

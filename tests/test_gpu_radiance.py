@@ -280,3 +280,37 @@ def test_tms_corrected_radiances_vs_oracle(nstr):
     _, u0 = disort_rad_forward(prop, bc, nstr=nstr, nmom=nmom, umu=umu, phi=phi, utau=utau)
     assert _col_err(uu, uref) < TOL
     assert _col_err(uref, u0) > 1e-3   # the correction is not a no-op here
+
+
+@pytest.mark.parametrize("nstr", [16, 32])
+def test_ims_aureole_vs_oracle(nstr, monkeypatch):
+    """The IMS term of the Nakajima-Tanaka correction (STWL A.13-A.16) on
+    forward-peaked HG layers (g 0.8-0.9, 96 moments) seen in the aureole:
+    downward directions around the beam at depths inside and below the layers,
+    GPU vs the oracle (TMS + IMS); the IMS term itself is not negligible here."""
+    from oracle import disort_rad_np
+    rng = np.random.default_rng(700 + nstr)
+    nwave, ncol, nlyr, nmom = 2, 2, 3, 96
+    prop = np.zeros((nwave, ncol, nlyr, 2 + nmom))
+    prop[..., 0] = rng.uniform(0.05, 0.6, (nwave, ncol, nlyr))
+    prop[..., 1] = rng.uniform(0.9, 0.99, (nwave, ncol, nlyr))
+    g = rng.uniform(0.8, 0.9, (nwave, ncol, nlyr))
+    for l in range(nmom):
+        prop[..., 2 + l] = g ** (l + 1)
+    umu0 = rng.uniform(0.5, 0.7, (nwave, ncol))
+    bc = {"fbeam": np.ones((nwave, ncol)), "umu0": umu0, "phi0": np.zeros((nwave, ncol)),
+          "albedo": rng.uniform(0, 0.3, (nwave, ncol))}
+    total = prop[..., 0].sum(axis=-1).min()
+    utau = [0.0, 0.3 * total, 0.7 * total, total]
+    umu, phi = [-0.7, -0.62, -0.58, -0.5, 0.6], [0.0, 4.0, 15.0, 180.0]
+    d = _disort(nstr, nlyr, nwave, ncol, flags="usrtau,usrang,lamber,intensity_correction,"
+                "old_intensity_correction", umu=umu, phi=phi, utau=utau, nmom=nmom)
+    d.forward(torch.as_tensor(prop, device=DEV), _dev(bc))
+    uu = d.get_rad().cpu().numpy()
+    _, uref = disort_rad_forward(prop, bc, nstr=nstr, nmom=nmom, umu=umu, phi=phi, utau=utau,
+                                 corint=True)
+    assert _col_err(uu, uref) < TOL
+    monkeypatch.setattr(disort_rad_np, "ims_correction", lambda *a, **k: 0.0)
+    _, utms = disort_rad_forward(prop, bc, nstr=nstr, nmom=nmom, umu=umu, phi=phi, utau=utau,
+                                 corint=True)
+    assert _col_err(uref, utms) > 1e-4   # the IMS term is resolved by the comparison
