@@ -6,7 +6,7 @@ import bench
 dev = torch.device('cuda', 0)
 from pyharp_amd import Disort, DisortOptions
 nstr = int(os.environ.get("PMC_NSTR", "16"))
-W, C, L = (8, 8192, 80) if nstr <= 16 else (4, 4096, 80)
+W, C, L = (8, int(os.environ.get("PMC_C", "8192")), 80) if nstr <= 16 else (4, 4096, 80)
 kw = {} if nstr <= 16 else dict(ssa=(0.9, 0.9999), gasym=(0.6, 0.9), umu0=(0.1, 1.0))
 prop, bc, _ = bench.make_inputs(list(range(W)), C, L, nstr, False, dev, **kw)
 op = DisortOptions().flags('lamber,quiet,onlyfl').nwave(W).ncol(C)

@@ -186,6 +186,31 @@ def test_chunking_invariance():
     assert np.array_equal(f1, f2)
 
 
+@pytest.mark.parametrize("nstr,planck", [(16, False), (16, True), (8, False), (6, True)])
+def test_chunk_sizes_with_partial_waves(oracle_c, nstr, planck):
+    """4 x 65 = 260 solves as one chunk (last wave 4 lanes live), as two pipelined
+    chunks of 130 and as chunks of 17 give the same fluxes bit for bit, and match
+    the oracle."""
+    rng = np.random.default_rng(90 + nstr + planck)
+    prop, bc, kw = _random_batch(rng, 4, 65, 14, nstr, planck)
+    d = _disort(nstr, 14, 4, 65, planck=planck, wl=kw.get("wave_lower"),
+                wu=kw.get("wave_upper"))
+    from pyharp_amd.disort import _context
+    ctx = _context(0)
+    out = {}
+    for chunk in (0, 130, 17):
+        ctx.set_chunk(chunk)
+        try:
+            out[chunk] = _run(d, prop, bc, kw.get("temf"))
+        finally:
+            ctx.set_chunk(0)
+    assert np.array_equal(out[0], out[17])
+    assert np.array_equal(out[130], out[17])
+    ref = oracle_c.forward(prop, bc, kw.get("temf"), nstr=nstr, planck=planck,
+                           wave_lower=kw.get("wave_lower"), wave_upper=kw.get("wave_upper"))
+    assert rel_err(out[0], ref).max() < TOL
+
+
 def test_linearity_in_fbeam():
     rng = np.random.default_rng(8)
     prop, bc, _ = _random_batch(rng, 2, 16, 30, 16, False)
