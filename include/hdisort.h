@@ -151,6 +151,24 @@ int hd_solve_band(hd_context *ctx, const hd_config *cfg, const hd_inputs *in,
                   const hd_band *band, double *flux, int *status, void *stream);
 
 /*
+ * The same two solves on HOST arrays (pydisort's own contract: CPU tensors in,
+ * a CPU tensor out -- DisortImpl::forward [EXTERNAL] at
+ * examples/amars_sw.cpp:280, examples/amars_lw.cpp:80, tests/test_disort.cpp:49,
+ * src/radiation/radiation_band.cpp:124-127, all with CPU tensors).  Every
+ * hd_inputs pointer (and weight) is a host pointer; the arrays are copied to a
+ * device staging area of the context, solved on the device exactly as
+ * hd_solve / hd_solve_band, and flux / bflux / status copied back.  Synchronous;
+ * HD_ENUMERIC if any solve set an error bit (status, host int32[nwave*ncol],
+ * may be NULL).  No CPU arithmetic: without a device they fail as hd_solve does.
+ *   hd_solve_band_host: weight HOST [nwave]; bflux HOST [ncol][nlyr+1][2]
+ *   (required); flux HOST per-point fluxes or NULL.
+ */
+int hd_solve_host(hd_context *ctx, const hd_config *cfg, const hd_inputs *in, double *flux,
+                  int *status);
+int hd_solve_band_host(hd_context *ctx, const hd_config *cfg, const hd_inputs *in,
+                       const double *weight, double *bflux, double *flux, int *status);
+
+/*
  * Intensity path (flags usrtau / usrang, onlyfl off): pydisort's forward with
  * radiances and DisortImpl::get_rad [EXTERNAL], as called at
  * tests/test_disort.cpp:13-55 (user_mu, user_phi, user_tau; get_rad at :52)

@@ -25,8 +25,8 @@ HD_STATUS_ERROR_MASK = 0x0F
 # every symbol include/hdisort.h declares
 EXPORTED = ("hd_version", "hd_last_error", "hd_context_create", "hd_context_destroy",
             "hd_context_set_chunk", "hd_context_set_timing", "hd_context_get_timing",
-            "hd_context_reserve", "hd_solve", "hd_solve_band", "hd_solve_radiance",
-            "hd_quadrature")
+            "hd_context_reserve", "hd_solve", "hd_solve_band", "hd_solve_host",
+            "hd_solve_band_host", "hd_solve_radiance", "hd_quadrature")
 
 # every symbol include/hdharp.h declares (harp-side steps around the solve)
 HARP_EXPORTED = ("hd_attenuate", "hd_band_optics", "hd_rfm_attenuate", "hd_band_flux",
@@ -108,6 +108,11 @@ def load(path: str = LIB_PATH):
     lib.hd_solve_band.argtypes = [ctypes.c_void_p, ctypes.POINTER(HdConfig),
                                   ctypes.POINTER(HdInputs), ctypes.POINTER(HdBand),
                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.hd_solve_host.argtypes = [ctypes.c_void_p, ctypes.POINTER(HdConfig),
+                                  ctypes.POINTER(HdInputs), ctypes.c_void_p, ctypes.c_void_p]
+    lib.hd_solve_band_host.argtypes = [ctypes.c_void_p, ctypes.POINTER(HdConfig),
+                                       ctypes.POINTER(HdInputs), ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.hd_solve_radiance.argtypes = [ctypes.c_void_p, ctypes.POINTER(HdConfig),
                                       ctypes.POINTER(HdInputs), ctypes.POINTER(HdRadiance),
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

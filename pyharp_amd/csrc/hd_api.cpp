@@ -59,6 +59,10 @@ struct hd_context {
   std::mutex mu;
   hipEvent_t ev_done = nullptr;
   bool done_valid = false;
+  // hd_solve_host / hd_solve_band_host: device copies of the caller's host arrays
+  double* hstage = nullptr;
+  size_t hstage_len = 0;  // doubles
+  hipStream_t hstream = nullptr;
 };
 
 namespace {
@@ -335,6 +339,8 @@ int hd_context_destroy(hd_context* ctx) {
   (void)hipSetDevice(ctx->device);
   drain(ctx);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->hstage) (void)hipFree(ctx->hstage);
+  if (ctx->hstream) (void)hipStreamDestroy(ctx->hstream);
   if (ctx->status) (void)hipFree(ctx->status);
   if (ctx->anyerr) (void)hipFree(ctx->anyerr);
   for (int b = 0; b < 2; ++b) {
@@ -759,6 +765,118 @@ int hd_solve_band(hd_context* ctx, const hd_config* cfg, const hd_inputs* in,
   return run_solve(ctx, status, stream, "hd_solve_band", [&](int*& st, hipStream_t s) {
     return solve_enqueue(ctx, cfg, in, flux, band, st, s);
   });
+}
+
+}  // extern "C"
+
+namespace {
+
+// hd_solve_host / hd_solve_band_host: the same solve on the caller's host arrays
+// (pydisort's CPU-tensor contract).  The inputs go to a device staging area of
+// the context, the solve runs on the context's own stream, the outputs come back;
+// synchronous.  No CPU arithmetic: without a device the call fails like hd_solve.
+int solve_host(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double* flux,
+               const double* weight, double* bflux, int* status, const char* what) {
+  if (!ctx) return fail(nullptr, HD_EINVAL, "%s: null context", what);
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!cfg || !in) return fail(ctx, HD_EINVAL, "%s: null config or inputs", what);
+  const bool band = bflux != nullptr;
+  if (band && !weight) return fail(ctx, HD_EINVAL, "%s: band weights are required", what);
+  int rc = validate(ctx, cfg, in, flux ? flux : bflux);
+  if (rc) return rc;
+  const long nsolve = (long)in->nwave * in->ncol;
+  if (nsolve == 0) return HD_OK;
+  const bool planck = (cfg->flags & HD_FLAG_PLANCK) != 0;
+  const size_t nlev2 = 2 * (size_t)(cfg->nlyr + 1);
+  const size_t ns = (size_t)nsolve;
+  // layout: prop | 8 bc keys | temf | wave_lower | wave_upper | weight | flux | bflux | status
+  const double* bc_h[7] = {in->fbeam, in->umu0, in->albedo, in->btemp,
+                           in->ttemp, in->temis, in->fisot};
+  const size_t n_prop = ns * cfg->nlyr * (size_t)cfg->nprop;
+  const size_t n_temf = planck && in->temf ? (size_t)in->ncol * (cfg->nlyr + 1) : 0;
+  const size_t n_wave = planck && in->wave_lower ? (size_t)in->nwave : 0;
+  const size_t n_flux = flux ? ns * nlev2 : 0;
+  const size_t n_bflux = band ? (size_t)in->ncol * nlev2 : 0;
+  const size_t n_stat = (ns + 1) / 2;  // int32 in double slots
+  const size_t total = n_prop + 7 * ns + n_temf + 2 * n_wave + (band ? (size_t)in->nwave : 0) +
+                       n_flux + n_bflux + n_stat;
+  DeviceGuard guard;
+  HD_HIP(ctx, hipSetDevice(ctx->device));
+  if (!ctx->hstream) HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->hstream, hipStreamNonBlocking));
+  if (ctx->hstage_len < total) {
+    drain(ctx);
+    if (ctx->hstage) (void)hipFree(ctx->hstage);
+    ctx->hstage = nullptr;
+    ctx->hstage_len = 0;
+    if (hipMalloc(&ctx->hstage, total * sizeof(double)) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(ctx, HD_ENOMEM, "%s: cannot allocate %zu bytes of staging", what,
+                  total * sizeof(double));
+    }
+    ctx->hstage_len = total;
+  }
+  hipStream_t s = ctx->hstream;
+  double* q = ctx->hstage;
+  hipError_t copy_err = hipSuccess;
+  auto put = [&](const double* src, size_t n) -> const double* {
+    if (!src || n == 0) return nullptr;
+    double* d = q;
+    q += n;
+    // synchronous copies from the caller's (pageable) arrays: complete on return
+    const hipError_t e = hipMemcpy(d, src, n * sizeof(double), hipMemcpyHostToDevice);
+    if (e != hipSuccess && copy_err == hipSuccess) copy_err = e;
+    return d;
+  };
+  hd_inputs din = *in;
+  din.prop = put(in->prop, n_prop);
+  const double** bc_d[7] = {&din.fbeam, &din.umu0, &din.albedo, &din.btemp,
+                            &din.ttemp, &din.temis, &din.fisot};
+  for (int k = 0; k < 7; ++k) *bc_d[k] = put(bc_h[k], ns);
+  din.temf = put(n_temf ? in->temf : nullptr, n_temf);
+  din.wave_lower = put(n_wave ? in->wave_lower : nullptr, n_wave);
+  din.wave_upper = put(n_wave ? in->wave_upper : nullptr, n_wave);
+  const double* wd = band ? put(weight, (size_t)in->nwave) : nullptr;
+  if (copy_err != hipSuccess)
+    return fail(ctx, HD_EHIP, "%s: host->device copy: %s", what, hipGetErrorString(copy_err));
+  double* fd = flux ? q : nullptr;
+  q += n_flux;
+  double* bd = band ? q : nullptr;
+  q += n_bflux;
+  int* sd = reinterpret_cast<int*>(q);
+  rc = run_solve(ctx, sd, s, what, [&](int*& st, hipStream_t ss) {
+    if (!band) return solve_enqueue(ctx, cfg, &din, fd, nullptr, st, ss);
+    hd_band b{wd, bd};
+    return solve_enqueue(ctx, cfg, &din, fd, &b, st, ss);
+  });
+  if (rc) return rc;
+  std::vector<int> st_h(status ? 0 : ns);
+  int* st_out = status ? status : st_h.data();
+  HD_HIP(ctx, hipStreamSynchronize(s));
+  if (flux) HD_HIP(ctx, hipMemcpy(flux, fd, n_flux * sizeof(double), hipMemcpyDeviceToHost));
+  if (band) HD_HIP(ctx, hipMemcpy(bflux, bd, n_bflux * sizeof(double), hipMemcpyDeviceToHost));
+  HD_HIP(ctx, hipMemcpy(st_out, sd, ns * sizeof(int), hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < ns; ++i)
+    if (st_out[i] & HD_STATUS_ERROR_MASK)
+      return fail(ctx, HD_ENUMERIC,
+                  "%s: at least one solve failed (bad input, eigen breakdown or non-finite "
+                  "result); DisortWrapper::Run failed.", what);
+  return HD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hd_solve_host(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, double* flux,
+                  int* status) {
+  if (!flux) return fail(ctx, HD_EINVAL, "hd_solve_host: null flux");
+  return solve_host(ctx, cfg, in, flux, nullptr, nullptr, status, "hd_solve_host");
+}
+
+int hd_solve_band_host(hd_context* ctx, const hd_config* cfg, const hd_inputs* in,
+                       const double* weight, double* bflux, double* flux, int* status) {
+  if (!bflux) return fail(ctx, HD_EINVAL, "hd_solve_band_host: null bflux");
+  return solve_host(ctx, cfg, in, flux, weight, bflux, status, "hd_solve_band_host");
 }
 
 }  // extern "C"
