@@ -156,8 +156,10 @@ int hd_solve_band(hd_context *ctx, const hd_config *cfg, const hd_inputs *in,
  * examples/amars_sw.cpp:280, examples/amars_lw.cpp:80, tests/test_disort.cpp:49,
  * src/radiation/radiation_band.cpp:124-127, all with CPU tensors).  Every
  * hd_inputs pointer (and weight) is a host pointer; the arrays are copied to a
- * device staging area of the context, solved on the device exactly as
- * hd_solve / hd_solve_band, and flux / bflux / status copied back.  Synchronous;
+ * device staging area of the context in pieces of whole waves (~128 k solves;
+ * piece j+1's copy beside piece j's solve), each piece solved on the device
+ * exactly as hd_solve / hd_solve_band (the band sum: the pieces' partial sums
+ * added in piece order), and flux / bflux / status copied back.  Synchronous;
  * HD_ENUMERIC if any solve set an error bit (status, host int32[nwave*ncol],
  * may be NULL).  No CPU arithmetic: without a device they fail as hd_solve does.
  *   hd_solve_band_host: weight HOST [nwave]; bflux HOST [ncol][nlyr+1][2]

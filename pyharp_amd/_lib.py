@@ -201,6 +201,17 @@ class Context:
                                   ctypes.c_void_p(stream_ptr or 0))
         check(rc, self.handle)
 
+    def solve_host(self, cfg: HdConfig, inp: HdInputs, flux_ptr: int):
+        """hd_solve_host: every pointer a host address; synchronous."""
+        check(load().hd_solve_host(self.handle, ctypes.byref(cfg), ctypes.byref(inp),
+                                   ctypes.c_void_p(flux_ptr), None), self.handle)
+
+    def solve_band_host(self, cfg: HdConfig, inp: HdInputs, weight_ptr: int, bflux_ptr: int,
+                        flux_ptr: int | None):
+        check(load().hd_solve_band_host(self.handle, ctypes.byref(cfg), ctypes.byref(inp),
+                                        ctypes.c_void_p(weight_ptr), ctypes.c_void_p(bflux_ptr),
+                                        ctypes.c_void_p(flux_ptr or 0), None), self.handle)
+
     def solve_radiance(self, cfg: HdConfig, inp: HdInputs, rad: HdRadiance, flux_ptr: int,
                        uu_ptr: int | None, status_ptr: int | None, stream_ptr: int | None):
         rc = load().hd_solve_radiance(self.handle, ctypes.byref(cfg), ctypes.byref(inp),

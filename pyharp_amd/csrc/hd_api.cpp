@@ -17,6 +17,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/hdharp.h"
 #include "../../include/hdisort.h"
 #include "hd_kernels.hpp"
 #include "hd_rad.hpp"
@@ -62,7 +63,10 @@ struct hd_context {
   // hd_solve_host / hd_solve_band_host: device copies of the caller's host arrays
   double* hstage = nullptr;
   size_t hstage_len = 0;  // doubles
-  hipStream_t hstream = nullptr;
+  hipStream_t hstream = nullptr;   // host<->device copies
+  hipStream_t hstream2 = nullptr;  // the pieces' solves
+  hipEvent_t hev_in[2] = {nullptr, nullptr};
+  hipEvent_t hev_done[2] = {nullptr, nullptr};
 };
 
 namespace {
@@ -341,6 +345,11 @@ int hd_context_destroy(hd_context* ctx) {
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->hstage) (void)hipFree(ctx->hstage);
   if (ctx->hstream) (void)hipStreamDestroy(ctx->hstream);
+  if (ctx->hstream2) (void)hipStreamDestroy(ctx->hstream2);
+  for (int b = 0; b < 2; ++b) {
+    if (ctx->hev_in[b]) (void)hipEventDestroy(ctx->hev_in[b]);
+    if (ctx->hev_done[b]) (void)hipEventDestroy(ctx->hev_done[b]);
+  }
   if (ctx->status) (void)hipFree(ctx->status);
   if (ctx->anyerr) (void)hipFree(ctx->anyerr);
   for (int b = 0; b < 2; ++b) {
@@ -787,22 +796,38 @@ int solve_host(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, doubl
   const long nsolve = (long)in->nwave * in->ncol;
   if (nsolve == 0) return HD_OK;
   const bool planck = (cfg->flags & HD_FLAG_PLANCK) != 0;
-  const size_t nlev2 = 2 * (size_t)(cfg->nlyr + 1);
+  const int nlev = cfg->nlyr + 1;
+  const size_t nlev2 = 2 * (size_t)nlev;
   const size_t ns = (size_t)nsolve;
-  // layout: prop | 8 bc keys | temf | wave_lower | wave_upper | weight | flux | bflux | status
+  const size_t ncol = (size_t)in->ncol;
+  // Pieces of whole waves (contiguous slices of every input): piece j+1's arrays
+  // go over PCIe (copy stream) while piece j is solved (compute stream); two input
+  // buffers.  ~128 k solves per piece keeps each solve near full-batch efficiency.
+  const long wpp = std::max<long>(1, std::min<long>(in->nwave, (131072 + in->ncol - 1) / in->ncol));
+  const int npiece = (int)((in->nwave + wpp - 1) / wpp);
+  const size_t pin_prop = (size_t)wpp * ncol * cfg->nlyr * (size_t)cfg->nprop;
+  const size_t pin_bc = (size_t)wpp * ncol;
   const double* bc_h[7] = {in->fbeam, in->umu0, in->albedo, in->btemp,
                            in->ttemp, in->temis, in->fisot};
-  const size_t n_prop = ns * cfg->nlyr * (size_t)cfg->nprop;
-  const size_t n_temf = planck && in->temf ? (size_t)in->ncol * (cfg->nlyr + 1) : 0;
-  const size_t n_wave = planck && in->wave_lower ? (size_t)in->nwave : 0;
+  int nbc = 0;
+  for (int k = 0; k < 7; ++k) nbc += bc_h[k] != nullptr;
+  const size_t pin = pin_prop + nbc * pin_bc;
+  const size_t n_temf = planck ? ncol * nlev : 0;
+  const size_t n_wave = planck ? (size_t)in->nwave : 0;
+  const size_t n_w = band ? (size_t)in->nwave + npiece : 0;  // weights, then ones
   const size_t n_flux = flux ? ns * nlev2 : 0;
-  const size_t n_bflux = band ? (size_t)in->ncol * nlev2 : 0;
+  const size_t n_part = band ? (size_t)npiece * ncol * nlev2 + ncol * nlev2 : 0;
   const size_t n_stat = (ns + 1) / 2;  // int32 in double slots
-  const size_t total = n_prop + 7 * ns + n_temf + 2 * n_wave + (band ? (size_t)in->nwave : 0) +
-                       n_flux + n_bflux + n_stat;
+  const size_t total = 2 * pin + n_temf + 2 * n_wave + n_w + n_flux + n_part + n_stat;
   DeviceGuard guard;
   HD_HIP(ctx, hipSetDevice(ctx->device));
   if (!ctx->hstream) HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->hstream, hipStreamNonBlocking));
+  if (!ctx->hstream2) HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->hstream2, hipStreamNonBlocking));
+  for (int b = 0; b < 2; ++b) {
+    if (!ctx->hev_in[b]) HD_HIP(ctx, hipEventCreateWithFlags(&ctx->hev_in[b], hipEventDisableTiming));
+    if (!ctx->hev_done[b])
+      HD_HIP(ctx, hipEventCreateWithFlags(&ctx->hev_done[b], hipEventDisableTiming));
+  }
   if (ctx->hstage_len < total) {
     drain(ctx);
     if (ctx->hstage) (void)hipFree(ctx->hstage);
@@ -815,46 +840,97 @@ int solve_host(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, doubl
     }
     ctx->hstage_len = total;
   }
-  hipStream_t s = ctx->hstream;
+  hipStream_t cs = ctx->hstream, xs = ctx->hstream2;  // copies, solves
   double* q = ctx->hstage;
-  hipError_t copy_err = hipSuccess;
-  auto put = [&](const double* src, size_t n) -> const double* {
-    if (!src || n == 0) return nullptr;
-    double* d = q;
-    q += n;
-    // synchronous copies from the caller's (pageable) arrays: complete on return
-    const hipError_t e = hipMemcpy(d, src, n * sizeof(double), hipMemcpyHostToDevice);
-    if (e != hipSuccess && copy_err == hipSuccess) copy_err = e;
-    return d;
-  };
-  hd_inputs din = *in;
-  din.prop = put(in->prop, n_prop);
-  const double** bc_d[7] = {&din.fbeam, &din.umu0, &din.albedo, &din.btemp,
-                            &din.ttemp, &din.temis, &din.fisot};
-  for (int k = 0; k < 7; ++k) *bc_d[k] = put(bc_h[k], ns);
-  din.temf = put(n_temf ? in->temf : nullptr, n_temf);
-  din.wave_lower = put(n_wave ? in->wave_lower : nullptr, n_wave);
-  din.wave_upper = put(n_wave ? in->wave_upper : nullptr, n_wave);
-  const double* wd = band ? put(weight, (size_t)in->nwave) : nullptr;
-  if (copy_err != hipSuccess)
-    return fail(ctx, HD_EHIP, "%s: host->device copy: %s", what, hipGetErrorString(copy_err));
-  double* fd = flux ? q : nullptr;
+  double* inbuf[2] = {q, q + pin};
+  q += 2 * pin;
+  double* temf_d = n_temf ? q : nullptr;
+  q += n_temf;
+  double* wlo_d = n_wave ? q : nullptr;
+  q += n_wave;
+  double* whi_d = n_wave ? q : nullptr;
+  q += n_wave;
+  double* w_d = band ? q : nullptr;
+  q += n_w;
+  double* flux_d = flux ? q : nullptr;
   q += n_flux;
-  double* bd = band ? q : nullptr;
-  q += n_bflux;
-  int* sd = reinterpret_cast<int*>(q);
-  rc = run_solve(ctx, sd, s, what, [&](int*& st, hipStream_t ss) {
-    if (!band) return solve_enqueue(ctx, cfg, &din, fd, nullptr, st, ss);
-    hd_band b{wd, bd};
-    return solve_enqueue(ctx, cfg, &din, fd, &b, st, ss);
-  });
-  if (rc) return rc;
+  double* part_d = band ? q : nullptr;  // [piece][ncol][nlev][2], then the band sum
+  q += n_part;
+  int* st_d = reinterpret_cast<int*>(q);
+  auto h2d = [&](double* d, const double* h, size_t n) {
+    return hipMemcpyAsync(d, h, n * sizeof(double), hipMemcpyHostToDevice, cs);
+  };
+  if (n_temf) HD_HIP(ctx, h2d(temf_d, in->temf, n_temf));
+  if (n_wave) {
+    HD_HIP(ctx, h2d(wlo_d, in->wave_lower, n_wave));
+    HD_HIP(ctx, h2d(whi_d, in->wave_upper, n_wave));
+  }
+  if (band) {
+    HD_HIP(ctx, h2d(w_d, weight, (size_t)in->nwave));
+    std::vector<double> ones((size_t)npiece, 1.0);
+    HD_HIP(ctx, hipMemcpy(w_d + in->nwave, ones.data(), npiece * sizeof(double),
+                          hipMemcpyHostToDevice));
+  }
   std::vector<int> st_h(status ? 0 : ns);
   int* st_out = status ? status : st_h.data();
-  HD_HIP(ctx, hipStreamSynchronize(s));
-  if (flux) HD_HIP(ctx, hipMemcpy(flux, fd, n_flux * sizeof(double), hipMemcpyDeviceToHost));
-  if (band) HD_HIP(ctx, hipMemcpy(bflux, bd, n_bflux * sizeof(double), hipMemcpyDeviceToHost));
-  HD_HIP(ctx, hipMemcpy(st_out, sd, ns * sizeof(int), hipMemcpyDeviceToHost));
+  auto d2h = [&](int j) -> int {  // piece j's per-point fluxes and status, after its solve
+    const long w0 = (long)j * wpp, wj = std::min<long>(wpp, in->nwave - w0);
+    const size_t o = (size_t)w0 * ncol, n = (size_t)wj * ncol;
+    HD_HIP(ctx, hipStreamWaitEvent(cs, ctx->hev_done[j & 1], 0));
+    if (flux)
+      HD_HIP(ctx, hipMemcpyAsync(flux + o * nlev2, flux_d + o * nlev2, n * nlev2 * sizeof(double),
+                                 hipMemcpyDeviceToHost, cs));
+    HD_HIP(ctx, hipMemcpyAsync(st_out + o, st_d + o, n * sizeof(int), hipMemcpyDeviceToHost, cs));
+    return HD_OK;
+  };
+  for (int j = 0; j < npiece; ++j) {
+    const int b = j & 1;
+    const long w0 = (long)j * wpp, wj = std::min<long>(wpp, in->nwave - w0);
+    const size_t o = (size_t)w0 * ncol, n = (size_t)wj * ncol;
+    // buffer b was last read by the solve of piece j-2
+    if (j >= 2) HD_HIP(ctx, hipStreamWaitEvent(cs, ctx->hev_done[b], 0));
+    hd_inputs din = *in;
+    din.nwave = (int)wj;
+    double* p = inbuf[b];
+    const size_t nprop = n * cfg->nlyr * (size_t)cfg->nprop;
+    HD_HIP(ctx, h2d(p, in->prop + o * cfg->nlyr * (size_t)cfg->nprop, nprop));
+    din.prop = p;
+    p += nprop;
+    const double** bc_d[7] = {&din.fbeam, &din.umu0, &din.albedo, &din.btemp,
+                              &din.ttemp, &din.temis, &din.fisot};
+    for (int k = 0; k < 7; ++k) {
+      if (!bc_h[k]) continue;
+      HD_HIP(ctx, h2d(p, bc_h[k] + o, n));
+      *bc_d[k] = p;
+      p += n;
+    }
+    din.temf = temf_d;
+    din.wave_lower = wlo_d ? wlo_d + w0 : nullptr;
+    din.wave_upper = whi_d ? whi_d + w0 : nullptr;
+    HD_HIP(ctx, hipEventRecord(ctx->hev_in[b], cs));
+    HD_HIP(ctx, hipStreamWaitEvent(xs, ctx->hev_in[b], 0));
+    double* fd = flux ? flux_d + o * nlev2 : nullptr;
+    rc = run_solve(ctx, st_d + o, xs, what, [&](int*& st, hipStream_t ss) {
+      if (!band) return solve_enqueue(ctx, cfg, &din, fd, nullptr, st, ss);
+      hd_band bb{w_d + w0, part_d + (size_t)j * ncol * nlev2};
+      return solve_enqueue(ctx, cfg, &din, fd, &bb, st, ss);
+    });
+    if (rc) return rc;
+    HD_HIP(ctx, hipEventRecord(ctx->hev_done[b], xs));
+    if (j >= 1 && (rc = d2h(j - 1))) return rc;
+  }
+  if ((rc = d2h(npiece - 1))) return rc;
+  if (band) {
+    // the pieces' band partials, in piece (= wave) order
+    double* bsum = part_d + (size_t)npiece * ncol * nlev2;
+    rc = hd_band_flux(part_d, w_d + in->nwave, npiece, (int)ncol, nlev, bsum, xs);
+    if (rc) return rc;
+    HD_HIP(ctx, hipEventRecord(ctx->hev_done[0], xs));
+    HD_HIP(ctx, hipStreamWaitEvent(cs, ctx->hev_done[0], 0));
+    HD_HIP(ctx, hipMemcpyAsync(bflux, bsum, ncol * nlev2 * sizeof(double), hipMemcpyDeviceToHost, cs));
+  }
+  HD_HIP(ctx, hipStreamSynchronize(cs));
+  HD_HIP(ctx, hipStreamSynchronize(xs));
   for (size_t i = 0; i < ns; ++i)
     if (st_out[i] & HD_STATUS_ERROR_MASK)
       return fail(ctx, HD_ENUMERIC,

@@ -239,6 +239,11 @@ class Disort(RTSolver):
         in_dev = prop.device
         dev = in_dev if in_dev.type == "cuda" else torch.device("cuda", int(op.device()))
         f64 = torch.float64
+        if in_dev.type != "cuda" and not self.radiance and out is None and status is None:
+            # pydisort's CPU-tensor contract: the library's host-array entry points
+            # (hd_solve_host / hd_solve_band_host) copy the arrays over in pieces
+            # beside the solve of the previous piece
+            return self._forward_host(prop, bc, temf, band, dev, nwave, ncol, nlyr, nprop)
 
         def dev_tensor(x, shape=None):
             if x is None:
@@ -333,6 +338,68 @@ class Disort(RTSolver):
             self._rad = self._rad.to(in_dev)
         if in_dev.type != "cuda":
             return flux.to(in_dev)
+        return flux
+
+    def _forward_host(self, prop, bc, temf, band, dev, nwave, ncol, nlyr, nprop):
+        ds = self.options.ds()
+        op = self.options
+        f64 = torch.float64
+
+        def host(x, shape=None):
+            if x is None:
+                return None
+            t = torch.as_tensor(x, dtype=f64, device="cpu")
+            if shape is not None and tuple(t.shape) != shape:
+                t = t.expand(shape)
+            return t.contiguous()
+
+        keep = [host(prop)]
+        bct = {}
+        for k in _BC_KEYS:
+            if k in bc and bc[k] is not None:
+                t = host(bc[k], (nwave, ncol))
+                if tuple(t.shape) != (nwave, ncol):
+                    raise RuntimeError(f"Disort.forward: bc['{k}'] must be (nwave, ncol)")
+                bct[k] = t
+                keep.append(t)
+        tf = wl = wu = None
+        if self.planck:
+            tf = host(temf)
+            if tuple(tf.shape) != (ncol, nlyr + 1):
+                raise RuntimeError(f"Disort.forward: temf must be (ncol, nlyr+1) = "
+                                   f"{(ncol, nlyr + 1)}, got {tuple(tf.shape)}")
+            wl = torch.tensor(op.wave_lower(), dtype=f64)
+            wu = torch.tensor(op.wave_upper(), dtype=f64)
+            keep += [tf, wl, wu]
+
+        def ptr(t):
+            return t.data_ptr() if t is not None else None
+
+        cfg = _lib.HdConfig(nstr=ds.nstr, nmom=ds.nmom, nlyr=nlyr, nprop=nprop,
+                            flags=_lib.HD_FLAG_LAMBER | _lib.HD_FLAG_ONLYFL |
+                            (_lib.HD_FLAG_PLANCK if self.planck else 0))
+        inp = _lib.HdInputs(nwave=nwave, ncol=ncol, prop=ptr(keep[0]),
+                            fbeam=ptr(bct.get("fbeam")), umu0=ptr(bct.get("umu0")),
+                            albedo=ptr(bct.get("albedo")), btemp=ptr(bct.get("btemp")),
+                            ttemp=ptr(bct.get("ttemp")), temis=ptr(bct.get("temis")),
+                            fisot=ptr(bct.get("fisot")), temf=ptr(tf), wave_lower=ptr(wl),
+                            wave_upper=ptr(wu))
+        ctx = _context(dev.index)
+        if band is not None:
+            wts = host(band[0]).reshape(-1).contiguous()
+            if wts.numel() != nwave:
+                raise RuntimeError(f"Disort.forward_band: {wts.numel()} weights for {nwave} "
+                                   "waves")
+            bout = torch.empty((ncol, nlyr + 1, 2), dtype=f64)
+            with torch.cuda.device(dev):
+                ctx.solve_band_host(cfg, inp, wts.data_ptr(), bout.data_ptr(), None)
+            if band[1] is not None:
+                band[1].copy_(bout)
+                return band[1]
+            return bout
+        flux = torch.empty((nwave, ncol, nlyr + 1, 2), dtype=f64)
+        with torch.cuda.device(dev):
+            ctx.solve_host(cfg, inp, flux.data_ptr())
         return flux
 
     def _forward_radiance(self, cfg, inp, flux, status, stream, bc, dev, keep, nwave, ncol):

@@ -110,6 +110,33 @@ def test_solve_band_host_matches_oracle(hd, oracle_c, nstr, keep):
         assert rel_err(flux, ref).max() < TOL
 
 
+@pytest.mark.parametrize("band", [False, True])
+def test_host_pieces_pipeline(hd, oracle_c, band):
+    """Batches above ~128 k solves go over in pieces of whole waves (the copy of piece
+    j+1 beside the solve of piece j): 7 waves x 40 000 columns = three pieces, the
+    last one short; every solve of a sample and the band sum against the oracle."""
+    lib, ctx = hd
+    rng = np.random.default_rng(77 + band)
+    nwave, ncol, nlyr, nstr = 7, 40000, 6, 8
+    prop, bc, _ = _batch(rng, nwave, ncol, nlyr, nstr, False)
+    w = rng.uniform(0.1, 1.0, nwave) if band else None
+    rc, flux, bflux, status = _solve_host(lib, ctx, nstr, prop, bc, weight=w)
+    assert rc == 0, lib.hd_last_error(ctx)
+    assert not (status & 0x0F).any()
+    idx = rng.choice(nwave * ncol, 200, replace=False)
+    ref = np.zeros_like(flux)
+    for q in idx:
+        oracle_c.forward(prop, bc, nstr=nstr, first=int(q), count=1, out=ref)
+    got = flux.reshape(-1, nlyr + 1, 2)[idx]
+    assert rel_err(got, ref.reshape(-1, nlyr + 1, 2)[idx]).max() < TOL
+    if band:
+        cols = rng.choice(ncol, 20, replace=False)
+        sub = {k: v[:, cols] for k, v in bc.items()}
+        rsub = oracle_c.forward(np.ascontiguousarray(prop[:, cols]), sub, nstr=nstr)
+        bref = (rsub * w[:, None, None, None]).sum(axis=0)
+        assert np.abs(bflux[cols] - bref).max() <= 1e-9 * np.abs(bref).max()
+
+
 def test_solve_host_reports_bad_input(hd):
     from pyharp_amd import _lib
     lib, ctx = hd

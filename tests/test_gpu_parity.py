@@ -298,6 +298,29 @@ def test_cpu_tensors_round_trip(oracle_c):
     assert rel_err(out.numpy(), ref).max() < TOL
 
 
+@pytest.mark.parametrize("planck", [False, True])
+def test_cpu_tensors_band_and_planck(oracle_c, planck):
+    """CPU tensors go through the host-array entry points (hd_solve_host /
+    hd_solve_band_host): forward and forward_band against the oracle."""
+    rng = np.random.default_rng(13 + planck)
+    nwave, ncol, nlyr, nstr = 3, 5, 10, 8
+    prop, bc, kw = _random_batch(rng, nwave, ncol, nlyr, nstr, planck)
+    d = _disort(nstr, nlyr, nwave, ncol, planck=planck, wl=kw.get("wave_lower"),
+                wu=kw.get("wave_upper"))
+    pt = torch.as_tensor(prop)
+    bt = {k: torch.as_tensor(v) for k, v in bc.items()}
+    tt = None if not planck else torch.as_tensor(kw["temf"])
+    ref = oracle_c.forward(prop, bc, kw.get("temf"), nstr=nstr, planck=planck,
+                           wave_lower=kw.get("wave_lower"), wave_upper=kw.get("wave_upper"))
+    f = d.forward(pt, bt, tt)
+    assert f.device.type == "cpu" and rel_err(f.numpy(), ref).max() < TOL
+    w = rng.uniform(0.1, 1.0, nwave)
+    b = d.forward_band(pt, bt, tt, weights=torch.as_tensor(w))
+    assert b.device.type == "cpu"
+    bref = (ref * w[:, None, None, None]).sum(axis=0)
+    assert np.abs(b.numpy() - bref).max() <= 1e-9 * np.abs(bref).max()
+
+
 def test_cpp_dropin(oracle_c):
     """C++ libtorch module harp_amd::Disort (include/harp_amd/disort.hpp) used with
     the reference's SW call pattern; compiled by tests/cpp/build.sh."""
