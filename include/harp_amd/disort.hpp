@@ -243,6 +243,8 @@ class DisortImpl : public torch::nn::Cloneable<DisortImpl> {
                              uu.defined() ? uu.data_ptr<double>() : nullptr, nullptr,
                              reinterpret_cast<void*>(stream));
       rad_ = uu.defined() ? (x.in_dev.is_cuda() ? uu : uu.to(x.in_dev)) : uu;
+    } else if (x.host) {  // CPU tensors: hd_solve_host (pieces copied beside the solve)
+      rc = hd_solve_host(context(x.dev.index()), &x.cfg, &x.in, flux.data_ptr<double>(), nullptr);
     } else {
       rc = hd_solve(context(x.dev.index()), &x.cfg, &x.in, flux.data_ptr<double>(), nullptr,
                     reinterpret_cast<void*>(stream));
@@ -264,8 +266,11 @@ class DisortImpl : public torch::nn::Cloneable<DisortImpl> {
     auto bflux = torch::empty({x.ncol, x.nlyr + 1, 2}, x.f64);
     hd_band band{w.data_ptr<double>(), bflux.data_ptr<double>()};
     auto stream = at::hip::getCurrentHIPStream(x.dev.index()).stream();
-    const int rc = hd_solve_band(context(x.dev.index()), &x.cfg, &x.in, &band, nullptr, nullptr,
-                                 reinterpret_cast<void*>(stream));
+    const int rc =
+        x.host ? hd_solve_band_host(context(x.dev.index()), &x.cfg, &x.in, w.data_ptr<double>(),
+                                    bflux.data_ptr<double>(), nullptr, nullptr)
+               : hd_solve_band(context(x.dev.index()), &x.cfg, &x.in, &band, nullptr, nullptr,
+                               reinterpret_cast<void*>(stream));
     TORCH_CHECK(rc == HD_OK, "DisortWrapper::Run failed: ", hd_last_error(context(x.dev.index())));
     return x.in_dev.is_cuda() ? bflux : bflux.to(x.in_dev);
   }
@@ -283,6 +288,7 @@ class DisortImpl : public torch::nn::Cloneable<DisortImpl> {
   // hd_inputs pointers refer to)
   struct Batch {
     torch::Device dev = torch::kCPU, in_dev = torch::kCPU;
+    bool host = false;  // CPU tensors on the flux path: arrays stay on the host
     torch::TensorOptions f64;
     int nwave = 0, ncol = 0, nlyr = 0, nprop = 0;
     torch::Tensor p, tf, wl, wu;
@@ -313,7 +319,11 @@ class DisortImpl : public torch::nn::Cloneable<DisortImpl> {
                 options.wave_lower().size(), "/", options.wave_upper().size());
     x.in_dev = prop.device();
     x.dev = x.in_dev.is_cuda() ? x.in_dev : torch::Device(torch::kCUDA, options.device());
-    x.f64 = torch::TensorOptions().dtype(torch::kFloat64).device(x.dev);
+    // pydisort's callers hand over CPU tensors (amars_sw.cpp:280, amars_lw.cpp:80,
+    // radiation_band.cpp:124-127): on the flux path they go to the host-array entry
+    // points, which copy them over in pieces beside the solve
+    x.host = !x.in_dev.is_cuda() && !radiance_;
+    x.f64 = torch::TensorOptions().dtype(torch::kFloat64).device(x.host ? x.in_dev : x.dev);
     auto to_dev = [&](torch::Tensor t) { return t.to(x.f64).contiguous(); };
     x.p = to_dev(prop);
     static const char* keys[] = {"fbeam", "umu0", "albedo", "btemp", "ttemp", "temis", "fisot"};
