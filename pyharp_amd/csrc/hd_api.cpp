@@ -841,6 +841,15 @@ int solve_host(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, doubl
     ctx->hstage_len = total;
   }
   hipStream_t cs = ctx->hstream, xs = ctx->hstream2;  // copies, solves
+  // whatever happens below, nothing may still be reading or writing the
+  // caller's arrays when this returns
+  struct Drain {
+    hipStream_t a, b;
+    ~Drain() {
+      (void)hipStreamSynchronize(a);
+      (void)hipStreamSynchronize(b);
+    }
+  } drain_on_exit{cs, xs};
   double* q = ctx->hstage;
   double* inbuf[2] = {q, q + pin};
   q += 2 * pin;
