@@ -699,7 +699,15 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
         HD_HIP(ctx, hipEventRecord(ctx->ev_pro[buf ^ 1], ctx->side));
       }
       HD_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_sweep[buf], 0));
-      e = hd::launch_backsub_nn(nn, sa, ctx->side, s1 >= nsolve);  // last chunk: tail kernel
+      // The last chunk's back-substitution takes the uncapped tail kernel (nothing
+      // overlaps it).  With at most three chunks every chunk's does: the capped
+      // kernel then still runs beside the last layer kernel when the step could
+      // end, while the tail kernel takes the SIMDs briefly and is done -- 8-GPU
+      // rank shape (80 000 solves, 2 chunks) 9.47 -> 10.50 M solves/s, 4-GPU
+      // (160 000, 3 chunks) 10.0 -> 10.3 M; with 5 and 10 chunks the capped kernel
+      // hidden under the next layer kernel stays ahead (profiles/r02_tail_ab/)
+      const bool tail = s1 >= nsolve || (nsolve + chunk - 1) / chunk <= 3;
+      e = hd::launch_backsub_nn(nn, sa, ctx->side, tail);
       if (e == hipSuccess && band) e = hd::launch_band_reduce(band_args(s0, nsc), ctx->side);
       if (e != hipSuccess)
         return fail(ctx, HD_EHIP, "hd_solve: back-substitution launch failed: %s",
