@@ -6,6 +6,7 @@ north-star bound max |dF|/F < 1e-6 (metric in tests/helpers.py).
 """
 
 import math
+import os
 
 import numpy as np
 import pytest
@@ -479,3 +480,38 @@ def test_planck_edge_cases(oracle_c, nstr):
     d = _disort(nstr, nlyr, 1, 6, planck=True, wl=wl, wu=wu)
     f = _run(d, prop, bc, temf)
     assert rel_err(f, ref).max() < TOL
+
+
+def test_full_c4_size_properties(oracle_c):
+    """BASELINE's headline size (1e4 columns x 64 g-points, nstr 16, nlyr 80: 640 000
+    solves, the bench's inputs) through size-independent properties: the band sum of
+    forward_band equals the weighted sum of forward's per-point fluxes, the fluxes are
+    linear in fbeam, and a 256-solve sample matches the CPU oracle."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    dev = torch.device("cuda", 0)
+    W, C, L, nstr = 64, 10000, 80, 16
+    prop, bc, _ = bench.make_inputs(list(range(W)), C, L, nstr, False, dev)
+    d = _disort(nstr, L, W, C)
+    w = torch.linspace(0.5, 1.5, W, dtype=torch.float64, device=dev)
+    f = d.forward(prop, bc)
+    band = d.forward_band(prop, bc, weights=w)
+    ref_band = (f * w.view(-1, 1, 1, 1)).sum(0)
+    scale = ref_band.abs().amax()
+    err_sum = ((band - ref_band).abs().amax() / scale).item()
+    assert err_sum < 1e-13, err_sum
+    # linearity holds to rounding of the (nstr x nlyr) solve: 1.9e-12 observed
+    bc3 = dict(bc, fbeam=bc["fbeam"] * 3.0)
+    band3 = d.forward_band(prop, bc3, weights=w)
+    err_lin = ((band3 - 3.0 * band).abs().amax() / (3.0 * scale)).item()
+    assert err_lin < 1e-10, err_lin
+    rng = np.random.default_rng(4)
+    idx = rng.choice(W * C, 256, replace=False)
+    pn = prop.cpu().numpy()
+    bn = {k: v.cpu().numpy() for k, v in bc.items()}
+    ref = np.zeros((W, C, L + 1, 2))
+    for q in idx:
+        oracle_c.forward(pn, bn, nstr=nstr, first=int(q), count=1, out=ref)
+    got = f.cpu().numpy().reshape(-1, L + 1, 2)[idx]
+    assert rel_err(got, ref.reshape(-1, L + 1, 2)[idx]).max() < TOL
