@@ -20,6 +20,8 @@ so a convention shared by the oracle and the kernels cannot hide in them:
 * layer splitting -- the discrete-ordinate solution inside a homogeneous layer is
   exact in tau, so splitting every layer into two halves (same omega, moments)
   leaves the fluxes at the original levels unchanged (beam + Lambert surface).
+* the intensity path in isothermal equilibrium -- I = B(T) at every user depth,
+  user angle (off the quadrature nodes) and azimuth.
 """
 
 import math
@@ -113,3 +115,35 @@ def test_layer_split_invariance(nstr):
     scale = np.abs(fc).max(axis=(2, 3), keepdims=True)
     err = np.abs(ff[:, :, ::2] - fc) / scale
     assert err.max() < 1e-9, err.max()
+
+
+@pytest.mark.parametrize("nstr", [4, 16, 24])
+def test_isothermal_equilibrium_radiances(nstr):
+    """Intensity path (every azimuthal mode, user depths and user angles off the
+    quadrature nodes): in isothermal equilibrium I = B(T) at every depth, angle and
+    azimuth -- the user-angle source integrates the phase function over the nodes
+    exactly, so the radiances, not only the fluxes, are B to rounding."""
+    from pyharp_amd import Disort, DisortOptions
+    rng = np.random.default_rng(700 + nstr)
+    nwave, ncol, nlyr, T = 2, 4, 8, 245.0
+    prop = _random_layers(rng, nwave, ncol, nlyr, nstr)
+    wl, wu = np.array([300.0, 1200.0]), np.array([700.0, 1400.0])
+    total = prop[..., 0].sum(axis=-1).min()
+    utau = [0.0, 0.3 * total, total]
+    umu, phi = [-1.0, -0.6, -0.15, 0.1, 0.45, 0.8], [0.0, 75.0, 180.0]
+    op = DisortOptions().flags("usrtau,usrang,lamber,quiet,planck").nwave(nwave).ncol(ncol)
+    op.wave_lower(list(wl)).wave_upper(list(wu)).user_mu(umu).user_phi(phi).user_tau(utau)
+    op.ds().nlyr = nlyr
+    op.ds().nstr = nstr
+    op.ds().nmom = nstr
+    d = Disort(op)
+    bc = {"albedo": rng.uniform(0.0, 1.0, (nwave, ncol)),
+          "btemp": np.full((nwave, ncol), T), "ttemp": np.full((nwave, ncol), T),
+          "temis": np.ones((nwave, ncol))}
+    f = _run(d, prop, bc, np.full((ncol, nlyr + 1), T))
+    uu = d.get_rad().cpu().numpy()
+    for w in range(nwave):
+        b = _planck_band(wl[w], wu[w], T)
+        assert np.abs(uu[w] / uu[w].mean() - 1.0).max() < 1e-9
+        assert abs(uu[w].mean() / b - 1.0) < 2e-6
+        assert np.abs(f[w] / (math.pi * uu[w].mean()) - 1.0).max() < 1e-9
