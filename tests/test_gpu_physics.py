@@ -22,6 +22,7 @@ so a convention shared by the oracle and the kernels cannot hide in them:
   leaves the fluxes at the original levels unchanged (beam + Lambert surface).
 * the intensity path in isothermal equilibrium -- I = B(T) at every user depth,
   user angle (off the quadrature nodes) and azimuth.
+* superposition of sources -- beam + thermal = beam alone + thermal alone.
 """
 
 import math
@@ -147,3 +148,27 @@ def test_isothermal_equilibrium_radiances(nstr):
         assert np.abs(uu[w] / uu[w].mean() - 1.0).max() < 1e-9
         assert abs(uu[w].mean() / b - 1.0) < 2e-6
         assert np.abs(f[w] / (math.pi * uu[w].mean()) - 1.0).max() < 1e-9
+
+
+@pytest.mark.parametrize("nstr", [8, 16, 32])
+def test_source_superposition(nstr):
+    """The equations are linear in their sources: fluxes with beam + thermal
+    emission (layers, surface, top) = beam alone + thermal alone."""
+    rng = np.random.default_rng(800 + nstr)
+    nwave, ncol, nlyr = 2, 16, 20
+    prop = _random_layers(rng, nwave, ncol, nlyr, nstr)
+    wl, wu = np.array([400.0, 900.0]), np.array([650.0, 1300.0])
+    temf = np.linspace(290.0, 180.0, nlyr + 1)[None, :] + rng.uniform(-5, 5, (ncol, nlyr + 1))
+    alb = rng.uniform(0.0, 1.0, (nwave, ncol))
+    beam = {"fbeam": rng.uniform(1.0, 50.0, (nwave, ncol)),
+            "umu0": rng.uniform(0.1, 1.0, (nwave, ncol))}
+    therm = {"btemp": np.full((nwave, ncol), 295.0), "ttemp": np.full((nwave, ncol), 170.0),
+             "temis": np.full((nwave, ncol), 0.4)}
+    d = _disort(nstr, nlyr, nwave, ncol, planck=True, wl=wl, wu=wu)
+    both = _run(d, prop, dict(albedo=alb, **beam, **therm), temf)
+    fb = _run(d, prop, dict(albedo=alb, **beam, btemp=np.zeros((nwave, ncol))),
+              np.zeros_like(temf))
+    ft = _run(d, prop, dict(albedo=alb, **therm), temf)
+    scale = np.abs(both).max(axis=(2, 3), keepdims=True)
+    err = np.abs(both - (fb + ft)) / scale
+    assert err.max() < 1e-10, err.max()
