@@ -43,3 +43,23 @@ def test_oracle_layer_split_invariance(oracle_c, nstr):
     ff = oracle_c.forward(fine, bc, nstr=nstr)
     scale = np.abs(fc).max(axis=(2, 3), keepdims=True)
     assert (np.abs(ff[:, :, ::2] - fc) / scale).max() < 1e-9
+
+
+def test_oracle_source_superposition(oracle_c):
+    rng = np.random.default_rng(900)
+    nwave, ncol, nlyr, nstr = 1, 4, 8, 16
+    prop = _random_layers(rng, nwave, ncol, nlyr, nstr)
+    wl, wu = np.array([400.0]), np.array([650.0])
+    temf = np.linspace(290.0, 180.0, nlyr + 1)[None, :] + rng.uniform(-5, 5, (ncol, nlyr + 1))
+    alb = rng.uniform(0.0, 1.0, (nwave, ncol))
+    beam = {"fbeam": rng.uniform(1.0, 50.0, (nwave, ncol)),
+            "umu0": rng.uniform(0.1, 1.0, (nwave, ncol))}
+    therm = {"btemp": np.full((nwave, ncol), 295.0), "ttemp": np.full((nwave, ncol), 170.0),
+             "temis": np.full((nwave, ncol), 0.4)}
+    kw = dict(nstr=nstr, planck=True, wave_lower=wl, wave_upper=wu)
+    both = oracle_c.forward(prop, dict(albedo=alb, **beam, **therm), temf, **kw)
+    fb = oracle_c.forward(prop, dict(albedo=alb, **beam, btemp=np.zeros((nwave, ncol))),
+                          np.zeros_like(temf), **kw)
+    ft = oracle_c.forward(prop, dict(albedo=alb, **therm), temf, **kw)
+    scale = np.abs(both).max(axis=(2, 3), keepdims=True)
+    assert (np.abs(both - (fb + ft)) / scale).max() < 1e-10
