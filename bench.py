@@ -8,9 +8,15 @@ configuration the metric is quoted on): 1e4 synthetic columns x 64 g-points,
 nstr=16, nmom=16 (Henyey-Greenstein chi_l = g^l), nlyr=80, tau log-uniform
 [1e-5, 5], omega in [0, 0.99], g in [0, 0.85], umu0 in [0.05, 1], albedo in
 [0, 1], fbeam = 1 (``--planck`` adds thermal emission, T 150-300 K).
-``--config c5`` is SURVEY 8(d) "C5 aerosol" (BASELINE.json configs[4]):
-1e3 columns x 64 g-points, nstr=32, nmom=32, nlyr=80, omega in [0.9, 0.9999],
-g in [0.6, 0.9] (delta-M active), umu0 in [0.1, 1].
+``--config c5`` is SURVEY 8(d) "C5 aerosol" (BASELINE.json configs[4], "h2so4 +
+s8_k_fuller phase moments"): 1e3 columns x 64 spectral points, nstr=32, nmom=32,
+nlyr=80, umu0 in [0.1, 1]; prop is assembled on the device (untimed) by the
+band loop's mixing (hd_band_loop_optics, radiation_band.cpp:86-116) from the
+reference's s8_k_fuller.txt and h2so4.txt tables with Henyey-Greenstein
+asymmetry tables (g 0.6-0.85 for S8, 0.75 for H2SO4: the tables carry none),
+the amars_sw aerosol profile regridded to 80 layers and scaled per column.
+``--config c5s`` is the round-1/2 synthetic C5 (omega in [0.9, 0.9999], g in
+[0.6, 0.9]).
 One step = one flux solve of every (g-point, column) pair of the rank's shard
 + the g-weighted band flux (C, L+1, 2) -- fused into the solve
 (hd_solve_band: the per-g fluxes are never stored; ``--no-fuse`` = hd_solve
@@ -67,8 +73,10 @@ CONFIGS = {
     # name: ncol, ngpoint, nstr, nlyr, (ssa lo, hi), (g lo, hi), (umu0 lo, hi), label
     "c4": dict(ncol=10000, ngpoint=64, nstr=16, nlyr=80, ssa=(0.0, 0.99), g=(0.0, 0.85),
                umu0=(0.05, 1.0), label="C4 GCM batch"),
-    "c5": dict(ncol=1000, ngpoint=64, nstr=32, nlyr=80, ssa=(0.9, 0.9999), g=(0.6, 0.9),
-               umu0=(0.1, 1.0), label="C5 high-scatter aerosol"),
+    "c5": dict(ncol=1000, ngpoint=64, nstr=32, nlyr=80, aerosol=True, umu0=(0.1, 1.0),
+               label="C5 high-scatter aerosol (s8 + h2so4 band-loop optics, HG moments)"),
+    "c5s": dict(ncol=1000, ngpoint=64, nstr=32, nlyr=80, ssa=(0.9, 0.9999), g=(0.6, 0.9),
+                umu0=(0.1, 1.0), label="C5 high-scatter aerosol (synthetic omega, HG g)"),
     # thermal, non-scattering (SURVEY 8(d) C1 amars_lw ck and C3 line-by-line)
     "c1": dict(ncol=1, ngpoint=16, nstr=8, nlyr=40, lw=True, tau=(1e-4, 20.0), band=(1.0, 150.0),
                label="C1 amars_lw ck (synthetic k)"),
@@ -136,6 +144,42 @@ def make_inputs(gpoints, ncol, nlyr, nstr, planck, dev, seed=20250217, ssa=(0.0,
     return prop, bc, temf
 
 
+def make_aerosol_inputs(gpoints, ngpoint, ncol, nlyr, nstr, dev, seed=20250217,
+                        umu0=(0.1, 1.0)):
+    """C5 through the band loop (hd_band_loop_optics, radiation_band.cpp:86-116): S8 and
+    H2SO4 from the reference's tables (tests/golden/data, the reference's data/), HG
+    asymmetry tables, the amars_sw aerosol profile on nlyr layers with a per-column
+    concentration scale log-uniform in [0.3, 30]; spectral point g = wavenumber
+    linspace(2000, 50000, ngpoint)[g] (the amars_sw band)."""
+    from examples.amars_sw import atmosphere
+    from pyharp_amd.opacity import (AttenuatorOptions, H2SO4Simple, S8Fuller,
+                                    add_resource_directory, band_loop_optics)
+    add_resource_directory(os.path.join(ROOT, "tests", "golden", "data"))
+    op = AttenuatorOptions().species_names(["S8", "H2SO4"]).species_weights([256.e-3, 98.e-3])
+    s8 = S8Fuller(op.copy().species_ids([0]).opacity_files(["s8_k_fuller.txt"]))
+    h2 = H2SO4Simple(op.copy().species_ids([1]).opacity_files(["h2so4.txt"]))
+    s8.set_asymmetry(np.linspace(0.6, 0.85, s8.kwave.numel()))
+    h2.set_asymmetry(0.75)
+    conc0, _, dz, _ = atmosphere(nlyr)
+    rng = np.random.default_rng(seed)
+    scale = 10.0 ** rng.uniform(np.log10(0.3), np.log10(30.0), (ncol, 1, 1))
+    conc = torch.as_tensor(conc0 * scale, device=dev)
+    wave = np.linspace(2000.0, 50000.0, ngpoint)[list(gpoints)]
+    prop = band_loop_optics([s8, h2], conc, torch.as_tensor(dz, device=dev),
+                            {"wavenumber": torch.as_tensor(wave, device=dev)}, nstr)
+    W = len(gpoints)
+    f64 = torch.float64
+    bc = {k: torch.empty((W, ncol), dtype=f64, device=dev) for k in ("fbeam", "umu0", "albedo")}
+    for i, g in enumerate(gpoints):
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(seed * 1000 + int(g))
+        r = torch.rand((2, ncol), generator=gen, dtype=f64, device=dev)
+        bc["fbeam"][i] = 1.0
+        bc["umu0"][i] = umu0[0] + (umu0[1] - umu0[0]) * r[0]
+        bc["albedo"][i] = r[1]
+    return prop, bc, None
+
+
 def gpoint_weights(ngpoint):
     # fixed synthetic correlated-k weights (sum to 1)
     x = np.arange(ngpoint, dtype=np.float64)
@@ -154,18 +198,18 @@ def wave_bounds(ngpoint, band=None, ck=False):
 
 
 def load_pmc(nstr: int, nlyr: int, planck: bool):
-    """Measured HBM bytes per solve per kernel (profiles/pmc_latest.json, scripts/pmc_summarize.py)."""
-    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
-    if not os.path.exists(p):
-        return None
-    try:
-        with open(p) as f:
-            d = json.load(f)
-    except (OSError, ValueError):
-        return None
-    if (d.get("nstr"), d.get("nlyr"), bool(d.get("planck"))) != (nstr, nlyr, bool(planck)):
-        return None
-    return d
+    """Measured HBM bytes per solve per kernel for this shape: the profiles/pmc_*.json
+    (scripts/pmc_summarize.py) whose (nstr, nlyr, planck) match."""
+    import glob
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
+        try:
+            with open(p) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if (d.get("nstr"), d.get("nlyr"), bool(d.get("planck"))) == (nstr, nlyr, bool(planck)):
+            return d
+    return None
 
 
 def _cpu_model():
@@ -312,6 +356,9 @@ def main():
     if lw:
         prop, bc, temf = make_lw_inputs(gpoints, G, ncol, nlyr, nstr, cfgd["band"], cfgd["tau"],
                                         dev)
+    elif cfgd.get("aerosol"):
+        prop, bc, temf = make_aerosol_inputs(gpoints, G, ncol, nlyr, nstr, dev,
+                                             umu0=cfgd["umu0"])
     else:
         prop, bc, temf = make_inputs(gpoints, ncol, nlyr, nstr, args.planck, dev,
                                      ssa=cfgd["ssa"], gasym=cfgd["g"], umu0=cfgd["umu0"])
@@ -458,11 +505,14 @@ def main():
         max_err = None
         fused_vs_unfused = None
         if fuse and world == 1:
-            # per-g fluxes (untimed) for the parity checks; the fused band against
+            # per-g fluxes (untimed) for the parity checks, from the timed step's own
+            # kernel schedule (hd_solve_band with the per-point fluxes kept: bitwise
+            # hd_solve's, tests/test_gpu_band.py), so that a rocprofv3 trace of this
+            # command averages launches of one kind; the fused band against
             # hd_band_flux over them (only the summation order differs)
             band_fused = band.clone()
             flux = torch.empty((W, ncol, nlyr + 1, 2), dtype=torch.float64, device=dev)
-            disort.forward(prop, bc, temf, status=status, out=flux)
+            disort.forward_band(prop, bc, temf, weights=wts, flux=flux, status=status)
             bunf = band_flux(flux, wts)
             fused_vs_unfused = float(((band_fused - bunf).abs().max() /
                                       bunf.abs().max()).item())

@@ -241,6 +241,38 @@ torch::Tensor band_optics_of(torch::Tensor conc, torch::Tensor dz,
   return band_optics({mods->table(dev)...}, conc, dz, kwargs, nprop);
 }
 
+//! prop (nwave, ncol, nlyr, 2 + nmom) by RadiationBandImpl::forward's mixing
+//! (src/radiation/radiation_band.cpp:86-116): tau-weighted ssa, tau*ssa-weighted
+//! Henyey-Greenstein moments, the +1e-10 regularisation, tau = ext dz (hdharp.h
+//! hd_band_loop_optics).  atts: {module->table(device), gasym device pointer or
+//! nullptr}; ext0: (nwave, ncol, nlyr[, 1]) extinction of attenuators without ssa
+//! (an RFM forward), or undefined.
+inline torch::Tensor band_loop_optics(std::vector<hd_band_attenuator> const& atts,
+                                      torch::Tensor conc, torch::Tensor dz,
+                                      std::map<std::string, torch::Tensor> const& kwargs,
+                                      int nmom, torch::Tensor ext0 = {}) {
+  auto [coord, kind] = detail::coord_of(kwargs);
+  auto dev = detail::device_of({conc, coord, dz});
+  auto o = torch::TensorOptions().dtype(torch::kFloat64).device(dev);
+  auto c = conc.to(o).contiguous();
+  const int ncol = c.size(0), nlyr = c.size(1), nsp = c.size(2);
+  auto d = dz.to(o).reshape({-1, nlyr}).expand({ncol, nlyr}).contiguous();
+  auto x = coord.to(o).contiguous().view({-1});
+  torch::Tensor e0;
+  if (ext0.defined()) {
+    e0 = ext0.to(o).contiguous();
+    TORCH_CHECK(e0.numel() == x.size(0) * ncol * nlyr, "band_loop_optics: ext0 size");
+  }
+  auto prop = torch::empty({x.size(0), ncol, nlyr, 2 + nmom}, o);
+  int rc = hd_band_loop_optics(atts.data(), (int)atts.size(),
+                               e0.defined() ? e0.data_ptr<double>() : nullptr,
+                               x.data_ptr<double>(), kind, (int)x.size(0), c.data_ptr<double>(),
+                               ncol, nlyr, nsp, d.data_ptr<double>(), nmom,
+                               prop.data_ptr<double>(), detail::stream_of(dev));
+  TORCH_CHECK(rc == HD_OK, "hd_band_loop_optics: ", hd_last_error(nullptr));
+  return prop;
+}
+
 // ---- RFM (src/opacity/rfm.hpp, rfm.cpp) -------------------------------------
 class RFMImpl : public torch::nn::Cloneable<RFMImpl> {
  public:

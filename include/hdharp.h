@@ -13,6 +13,9 @@
  *     hd_band_optics   the amars_sw assembly (examples/amars_sw.cpp:261-271):
  *                      sum of attenuators, x dz, ssa = sum(ssa k c)/sum(k c),
  *                      written as prop [nwave][ncol][nlyr][nprop]
+ *     hd_band_loop_optics  the library band loop's mixing (radiation_band.cpp:86-116):
+ *                      tau-weighted ssa, tau*ssa-weighted phase moments, the
+ *                      reference's +1e-10 regularisation
  *   after the solve -- band epilogue:
  *     hd_band_flux     sum_w weight_w F_w (examples/amars_lw.cpp:84-88;
  *                      amars_sw.cpp:169-196 with weight = d(wavenumber);
@@ -62,6 +65,35 @@ int hd_attenuate(const hd_attenuator *att, const double *coord, int coord_kind, 
 int hd_band_optics(const hd_attenuator *atts, int natt, const double *coord, int coord_kind,
                    int nwave, const double *conc, int ncol, int nlyr, int nspecies,
                    const double *dz, int nprop, double *prop, void *stream);
+
+/* RadiationBandImpl::forward's optics mixing (src/radiation/radiation_band.cpp:86-116,
+ * the "band loop") on the device, written straight into the solver layout
+ *   prop [nwave][ncol][nlyr][2+nmom].
+ * Each attenuator a contributes kdata_a = [k_a(lambda) c_a, ssa_a(lambda),
+ * chi_a1..chi_anmom] with Henyey-Greenstein moments chi_al = g_a(lambda)^l (k, ssa and
+ * g interpolated in wavelength as hd_attenuate does); per element, in this order
+ * (ext0 first, then the attenuators in array order; products left to right, no
+ * fused multiply-adds):
+ *   ext  = ext0 + sum_a k_a c_a                     (radiation_band.cpp:91)
+ *   sca  = sum_a ssa_a * (k_a c_a)                  (:94-96)
+ *   m_l  = sum_{a with g} (chi_al * ssa_a) * (k_a c_a)  (:98-103)
+ *   prop[2+l-1] = m_l / (sca + 1e-10)               (:108-110)
+ *   prop[1]     = sca / (ext + 1e-10)               (:112-114)
+ *   prop[0]     = ext * dz                          (:116)
+ * ext0: [nwave][ncol][nlyr] extinction of attenuators without ssa (nprop = 1, e.g.
+ * hd_rfm_attenuate's output), or NULL.  Latent reference bugs not reproduced
+ * (SURVEY.md 3.3): prop there lacks the wave axis (:83-84) and the aerosol
+ * modules' slot 1 is already ssa*k*c (s8_fuller.cpp:113-114), which the loop
+ * would weight by k*c a second time -- here slot 1 of an attenuator is its ssa. */
+typedef struct hd_band_attenuator {
+  hd_attenuator table;  /* k_ext, ssa vs wavelength (as hd_attenuate)               */
+  const double *gasym;  /* [table.nrow] HG asymmetry g(lambda), or NULL: no moments  */
+} hd_band_attenuator;
+
+int hd_band_loop_optics(const hd_band_attenuator *atts, int natt, const double *ext0,
+                        const double *coord, int coord_kind, int nwave, const double *conc,
+                        int ncol, int nlyr, int nspecies, const double *dz, int nmom,
+                        double *prop, void *stream);
 
 /* one RFM absorption table (harp::RFMImpl after reset(), src/opacity/rfm.cpp:30-120;
  * the reference reads it from netCDF: dims Wavenumber/Pressure/TempGrid, variables

@@ -20,7 +20,9 @@
  *         2.. = phase moments chi_1..chi_nmom (chi_0 = 1 implicit)
  *         (src/index.h:12-18, src/radiation/radiation_band.cpp:116)
  *   bc    per-solve arrays [nwave][ncol] f64 (NULL = default): fbeam (0),
- *         umu0 (1), albedo (0), btemp (0), ttemp (0), temis (0), fisot (0)
+ *         umu0 (1), albedo (0), btemp (0), ttemp (0), temis (0), fisot (0);
+ *         umu0 is floored at 1e-3 as harp's driver does
+ *         (src/rtsolver/rt_solver_disort.cpp_:80: umu0 = mu > 1e-3 ? mu : 1e-3)
  *         (src/radiation/radiation_band.hpp:74-77, amars_sw.cpp:276-278,
  *          amars_lw.cpp:73-74)
  *   temf  [ncol][nlyr+1] f64 level temperatures, level 0 = bottom (planck)
@@ -67,14 +69,16 @@ extern "C" {
 
 /* per-solve status bits (int32 per solve) */
 #define HD_STATUS_BAD_INPUT 0x01 /* tau<0, ssa outside [0,1], f>=1, umu0>1 ... */
-#define HD_STATUS_EIGEN 0x02     /* eigenvalue <= 0 / Cholesky breakdown         */
+#define HD_STATUS_EIGEN 0x02     /* eigenvalue <= 0 / Cholesky breakdown / Jacobi
+                                    not converged within the sweep cap          */
 #define HD_STATUS_NONFINITE 0x04 /* NaN/Inf produced                             */
 #define HD_STATUS_RESONANCE 0x10 /* warning: umu0 ~ 1/k (beam/quadrature resonance) */
 #define HD_STATUS_PIVOT 0x20     /* warning: tiny pivot in the boundary sweep      */
 #define HD_STATUS_ERROR_MASK 0x0F
 
 typedef struct hd_config {
-  int nstr;       /* number of streams, even, 2..32 */
+  int nstr;       /* number of streams, even, 2..32 (a limit of this boundary:
+                     nstr > 32 is rejected with HD_EINVAL) */
   int nmom;       /* phase moments the module was configured with (>= 0)   */
   int nlyr;       /* layers                                                 */
   int nprop;      /* last-dim size of prop (>= 1); moments used = min(nmom, nprop-2) */
@@ -101,15 +105,23 @@ typedef struct hd_timing {
 typedef struct hd_context hd_context;
 
 int hd_version(void);
-const char *hd_last_error(const hd_context *ctx); /* ctx may be NULL (global) */
+/* ctx may be NULL (the last error of any call).  The string is a copy owned by the
+ * calling thread, valid until that thread calls hd_last_error again. */
+const char *hd_last_error(const hd_context *ctx);
 
 int hd_context_create(hd_context **ctx, int device);
 int hd_context_destroy(hd_context *ctx);
 /* max solves per internal chunk (scratch = chunk*nlyr*~1.4 KB); 0 = auto */
 int hd_context_set_chunk(hd_context *ctx, long max_solves);
 int hd_context_set_timing(hd_context *ctx, int enable);
+/* debug: cap on the eigensolver's Jacobi sweeps (0 = default 16).  A solve whose
+ * Jacobi is still rotating at the cap sets HD_STATUS_EIGEN. */
+int hd_context_set_max_sweeps(hd_context *ctx, int max_sweeps);
 int hd_context_get_timing(const hd_context *ctx, hd_timing *out);
-/* pre-size scratch for graph capture / steady state */
+/* pre-size scratch for graph capture / steady state: room for hd_solve and for
+ * hd_solve_band (any nwave) of up to nsolve solves of this config, and the status
+ * buffer.  A call captured into a HIP graph never allocates: if scratch would
+ * have to grow during capture it returns HD_EINVAL instead. */
 int hd_context_reserve(hd_context *ctx, const hd_config *cfg, long nsolve);
 
 /*

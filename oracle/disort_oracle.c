@@ -622,7 +622,10 @@ long hdo_forward(int nwave, int ncol, int nlyr, int nprop, int nstr, int nmom, i
       hdo_column_in in;
       in.nstr = nstr; in.nlyr = nlyr; in.nmom = nm; in.planck = planck;
       in.dtauc = dtauc; in.ssalb = ssalb; in.pmom = pm; in.temper = tem;
-      in.umu0 = umu0 ? umu0[s] : 1.0;
+      /* harp's floor: ds_.bc.umu0 = mu > 1e-3 ? mu : 1e-3
+         (legacy src/rtsolver/rt_solver_disort.cpp_:80); NaN stays NaN */
+      in.umu0 = umu0 ? (umu0[s] > 1.0e-3 ? umu0[s] : (umu0[s] != umu0[s] ? umu0[s] : 1.0e-3))
+                     : 1.0;
       in.fbeam = fbeam ? fbeam[s] : 0.0;
       in.albedo = albedo ? albedo[s] : 0.0;
       in.fisot = fisot ? fisot[s] : 0.0;

@@ -57,7 +57,7 @@ import math
 import numpy as np
 import scipy.linalg
 
-from .disort_np import DITHER, double_gauss, legendre_table, plkavg, setdis, soleig, upisot
+from .disort_np import DITHER, double_gauss, legendre_table, plkavg, setdis, soleig, umu0_floor, upisot
 
 
 def lepoly(nstr: int, m: int, mu) -> np.ndarray:
@@ -498,6 +498,7 @@ def disort_rad_forward(prop, bc, temf=None, *, nstr, umu, phi, utau=None, nmom=N
     keys = dict(fbeam=0.0, umu0=1.0, phi0=0.0, albedo=0.0, btemp=0.0, ttemp=0.0, temis=0.0,
                 fisot=0.0)
     v = {k: bcv(k, d) for k, d in keys.items()}
+    v["umu0"] = umu0_floor(v["umu0"])  # harp's floor (rt_solver_disort.cpp_:80)
     umu = np.atleast_1d(np.asarray(umu, np.float64))
     phi = np.atleast_1d(np.asarray(phi, np.float64))
     flux = uu = None

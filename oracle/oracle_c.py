@@ -20,9 +20,9 @@ _dp = ctypes.POINTER(ctypes.c_double)
 
 
 def build(force: bool = False) -> str:
-    """Compile the C oracle with gcc (``make -C oracle``)."""
-    if force or not os.path.exists(LIB_PATH):
-        subprocess.run(["make", "-C", _HERE], check=True, capture_output=True)
+    """Compile the C oracle with gcc (``make -C oracle``; make skips an up-to-date build)."""
+    cmd = ["make", "-C", _HERE] + (["-B"] if force else [])
+    subprocess.run(cmd, check=True, capture_output=True)
     return LIB_PATH
 
 

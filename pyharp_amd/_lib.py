@@ -24,13 +24,14 @@ HD_STATUS_ERROR_MASK = 0x0F
 
 # every symbol include/hdisort.h declares
 EXPORTED = ("hd_version", "hd_last_error", "hd_context_create", "hd_context_destroy",
-            "hd_context_set_chunk", "hd_context_set_timing", "hd_context_get_timing",
+            "hd_context_set_chunk", "hd_context_set_timing", "hd_context_set_max_sweeps",
+            "hd_context_get_timing",
             "hd_context_reserve", "hd_solve", "hd_solve_band", "hd_solve_host",
             "hd_solve_band_host", "hd_solve_radiance", "hd_quadrature")
 
 # every symbol include/hdharp.h declares (harp-side steps around the solve)
-HARP_EXPORTED = ("hd_attenuate", "hd_band_optics", "hd_rfm_attenuate", "hd_band_flux",
-                 "hd_heating_rate", "hd_spherical_flux_correction")
+HARP_EXPORTED = ("hd_attenuate", "hd_band_optics", "hd_band_loop_optics", "hd_rfm_attenuate",
+                 "hd_band_flux", "hd_heating_rate", "hd_spherical_flux_correction")
 HD_COORD_WAVELENGTH, HD_COORD_WAVENUMBER = 0, 1
 
 # every symbol include/hdnc.h declares (netCDF readers, host code)
@@ -43,6 +44,10 @@ _dp = ctypes.c_void_p
 class HdAttenuator(ctypes.Structure):
     _fields_ = [("nrow", ctypes.c_int), ("wavelength", _dp), ("kext", _dp), ("ssa", _dp),
                 ("species", ctypes.c_int)]
+
+
+class HdBandAttenuator(ctypes.Structure):
+    _fields_ = [("table", HdAttenuator), ("gasym", _dp)]
 
 
 class HdRfmTable(ctypes.Structure):
@@ -101,6 +106,7 @@ def load(path: str = LIB_PATH):
     lib.hd_context_destroy.argtypes = [ctypes.c_void_p]
     lib.hd_context_set_chunk.argtypes = [ctypes.c_void_p, ctypes.c_long]
     lib.hd_context_set_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.hd_context_set_max_sweeps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.hd_context_get_timing.argtypes = [ctypes.c_void_p, ctypes.POINTER(HdTiming)]
     lib.hd_context_reserve.argtypes = [ctypes.c_void_p, ctypes.POINTER(HdConfig), ctypes.c_long]
     lib.hd_solve.argtypes = [ctypes.c_void_p, ctypes.POINTER(HdConfig), ctypes.POINTER(HdInputs),
@@ -124,6 +130,8 @@ def load(path: str = LIB_PATH):
                                  _dp]
     lib.hd_band_optics.argtypes = [ctypes.POINTER(HdAttenuator), ci, _dp, ci, ci, _dp, ci, ci, ci,
                                    _dp, ci, _dp, _dp]
+    lib.hd_band_loop_optics.argtypes = [ctypes.POINTER(HdBandAttenuator), ci, _dp, _dp, ci, ci,
+                                        _dp, ci, ci, ci, _dp, ci, _dp, _dp]
     lib.hd_rfm_attenuate.argtypes = [ctypes.POINTER(HdRfmTable), _dp, ci, ci, ci, _dp, _dp, _dp,
                                      _dp]
     lib.hd_band_flux.argtypes = [_dp, _dp, ci, ci, ci, _dp, _dp]
@@ -180,6 +188,15 @@ class Context:
 
     def set_timing(self, on: bool):
         check(load().hd_context_set_timing(self.handle, int(bool(on))), self.handle)
+
+    def reserve(self, cfg: HdConfig, nsolve: int):
+        """hd_context_reserve: size scratch (hd_solve and hd_solve_band) and status."""
+        check(load().hd_context_reserve(self.handle, ctypes.byref(cfg), int(nsolve)),
+              self.handle)
+
+    def set_max_sweeps(self, n: int):
+        """Debug: cap the eigensolver's Jacobi sweeps (0 = default)."""
+        check(load().hd_context_set_max_sweeps(self.handle, int(n)), self.handle)
 
     def timing(self) -> HdTiming:
         t = HdTiming()

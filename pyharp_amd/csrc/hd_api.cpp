@@ -34,9 +34,12 @@ struct hd_context {
   // timing: one event triple per launched chunk, resolved lazily in get_timing
   std::vector<hipEvent_t> pool;
   size_t pool_used = 0;
-  bool tables = false;
   hd_timing times{};
+  int max_sweeps = 16;  // Jacobi sweep cap (debug setter: hd_context_set_max_sweeps)
+  // true while a solve enqueues into a capturing stream: scratch may not grow then
+  bool capturing = false;
   std::string err;
+  std::mutex err_mu;  // guards err (hd_last_error reads it without the solve lock)
   // register path: back-substitution of chunk k on `side`, beside chunk k+1's
   // layer kernel (its 44-VGPR waves fit next to the layer kernel's on a SIMD)
   hipStream_t side = nullptr;
@@ -49,7 +52,6 @@ struct hd_context {
   hipEvent_t ev_pro[2] = {nullptr, nullptr};  // next chunk's prologue done (side stream)
   hipEvent_t ev_fork = nullptr;                // start of a solve on the caller's stream
   double* sink = nullptr;                      // team kernels: stores of lanes >= nstr/2
-  bool rad_tables = false;                     // intensity-path constants uploaded
   double* rad_grid = nullptr;                  // device copies of umu | phi | utau
   size_t rad_grid_len = 0;
   // Serialisation of the context's scratch (SURVEY 8(b) "Threading"): every
@@ -80,7 +82,10 @@ int fail(hd_context* ctx, int code, const char* fmt, ...) {
   va_start(ap, fmt);
   vsnprintf(buf, sizeof(buf), fmt, ap);
   va_end(ap);
-  if (ctx) ctx->err = buf;
+  if (ctx) {
+    std::lock_guard<std::mutex> lk(ctx->err_mu);
+    ctx->err = buf;
+  }
   std::lock_guard<std::mutex> lk(g_err_mu);
   g_err = buf;
   return code;
@@ -146,14 +151,45 @@ void make_quad(int nn, hd::QuadHost& q) {
   }
 }
 
-int ensure_tables(hd_context* ctx) {
-  if (ctx->tables) return HD_OK;
+// The quadrature tables of every nn, built once per process; their upload into a
+// device's __constant__ memory happens once per device (the module's constants
+// are per device, shared by every context on it), under one global lock.
+const hd::QuadHost* quad_host() {
   static hd::QuadHost all[hd::kMaxNN];
-  for (int nn = 1; nn <= hd::kMaxNN; ++nn) make_quad(nn, all[nn - 1]);
+  static std::once_flag once;
+  std::call_once(once, [] {
+    for (int nn = 1; nn <= hd::kMaxNN; ++nn) make_quad(nn, all[nn - 1]);
+  });
+  return all;
+}
+
+constexpr int kMaxDevices = 64;
+std::mutex g_tab_mu;
+bool g_tables[kMaxDevices] = {};      // flux-path tables uploaded, per device
+bool g_rad_tables[kMaxDevices] = {};  // intensity-path tables uploaded, per device
+
+int ensure_tables(hd_context* ctx) {
+  if (ctx->device < 0 || ctx->device >= kMaxDevices)
+    return fail(ctx, HD_EINVAL, "hd_solve: device %d beyond the table cache", ctx->device);
+  std::lock_guard<std::mutex> lk(g_tab_mu);
+  if (g_tables[ctx->device]) return HD_OK;
+  const hd::QuadHost* all = quad_host();
   hipError_t e = hd::upload_quad_tables(all);
   if (e == hipSuccess) e = hd::upload_quad_tables_team(all);
   if (e != hipSuccess) return fail(ctx, HD_EHIP, "hd_solve: constant upload: %s", hipGetErrorString(e));
-  ctx->tables = true;
+  g_tables[ctx->device] = true;
+  return HD_OK;
+}
+
+int ensure_rad_tables(hd_context* ctx) {
+  int rc = ensure_tables(ctx);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(g_tab_mu);
+  if (g_rad_tables[ctx->device]) return HD_OK;
+  hipError_t e = hd::upload_rad_tables(quad_host());
+  if (e != hipSuccess)
+    return fail(ctx, HD_EHIP, "hd_solve_radiance: constant upload: %s", hipGetErrorString(e));
+  g_rad_tables[ctx->device] = true;
   return HD_OK;
 }
 
@@ -182,8 +218,16 @@ void drain(hd_context* ctx) {
   if (ctx->done_valid) (void)hipEventSynchronize(ctx->ev_done);
 }
 
+// Growing a buffer frees the old one, which a captured graph may still point at,
+// and a free/malloc cannot be captured: during capture growth is an error (size
+// the context first with hd_context_reserve, or run the call once eagerly).
 int ensure_scratch(hd_context* ctx, size_t ndoubles) {
   if (ctx->scratch_doubles >= ndoubles) return HD_OK;
+  if (ctx->capturing)
+    return fail(ctx, HD_EINVAL,
+                "hd_solve: scratch must grow to %zu bytes inside a stream capture; size the "
+                "context first (hd_context_reserve, or one eager call of the same shape)",
+                ndoubles * sizeof(double));
   drain(ctx);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   ctx->scratch = nullptr;
@@ -199,6 +243,10 @@ int ensure_scratch(hd_context* ctx, size_t ndoubles) {
 
 int ensure_status(hd_context* ctx, size_t n) {
   if (ctx->status_len >= n) return HD_OK;
+  if (ctx->capturing)
+    return fail(ctx, HD_EINVAL,
+                "hd_solve: the status buffer must grow inside a stream capture; pass a status "
+                "buffer or size the context first (hd_context_reserve)");
   drain(ctx);
   if (ctx->status) (void)hipFree(ctx->status);
   ctx->status = nullptr;
@@ -298,11 +346,18 @@ extern "C" {
 
 int hd_version(void) { return HDISORT_VERSION; }
 
-const char* hd_last_error(const hd_context* ctx) {
-  if (ctx) return ctx->err.c_str();
-  std::lock_guard<std::mutex> lk(g_err_mu);
+// A copy per calling thread: valid until this thread's next hd_last_error call,
+// whatever other threads do to the context meanwhile.
+const char* hd_last_error(const hd_context* ctx_) {
   static thread_local std::string copy;
-  copy = g_err;
+  if (ctx_) {
+    hd_context* ctx = const_cast<hd_context*>(ctx_);
+    std::lock_guard<std::mutex> lk(ctx->err_mu);
+    copy = ctx->err;
+  } else {
+    std::lock_guard<std::mutex> lk(g_err_mu);
+    copy = g_err;
+  }
   return copy.c_str();
 }
 
@@ -320,18 +375,31 @@ int hd_context_create(hd_context** out, int device) {
                 ndev);
   hd_context* ctx = new hd_context();
   ctx->device = device;
-  HD_HIP(ctx, hipSetDevice(device));
-  HD_HIP(ctx, hipMalloc(&ctx->anyerr, sizeof(int)));
-  HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
-  HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->lay, hipStreamNonBlocking));
-  HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
-  HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming));
-  HD_HIP(ctx, hipMalloc(&ctx->sink, 4096 * sizeof(double)));
-  for (int b = 0; b < 2; ++b) {
-    HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_layer[b], hipEventDisableTiming));
-    HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_sweep[b], hipEventDisableTiming));
-    HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_back[b], hipEventDisableTiming));
-    HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_pro[b], hipEventDisableTiming));
+  auto init = [ctx]() -> int {
+    HD_HIP(ctx, hipSetDevice(ctx->device));
+    HD_HIP(ctx, hipMalloc(&ctx->anyerr, sizeof(int)));
+    HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+    HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->lay, hipStreamNonBlocking));
+    HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+    HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming));
+    HD_HIP(ctx, hipMalloc(&ctx->sink, 4096 * sizeof(double)));
+    for (int b = 0; b < 2; ++b) {
+      HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_layer[b], hipEventDisableTiming));
+      HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_sweep[b], hipEventDisableTiming));
+      HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_back[b], hipEventDisableTiming));
+      HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_pro[b], hipEventDisableTiming));
+    }
+    return HD_OK;
+  };
+  const int rc = init();
+  if (rc != HD_OK) {  // nothing leaks: destroy frees whatever init created
+    std::string msg;
+    {
+      std::lock_guard<std::mutex> lk(ctx->err_mu);
+      msg = ctx->err;
+    }
+    hd_context_destroy(ctx);
+    return fail(nullptr, rc, "%s", msg.c_str());
   }
   *out = ctx;
   return HD_OK;
@@ -377,6 +445,14 @@ int hd_context_set_chunk(hd_context* ctx, long max_solves) {
   return HD_OK;
 }
 
+int hd_context_set_max_sweeps(hd_context* ctx, int max_sweeps) {
+  if (!ctx || max_sweeps < 0 || max_sweeps > 64)
+    return fail(ctx, HD_EINVAL, "hd_context_set_max_sweeps: bad args");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->max_sweeps = max_sweeps > 0 ? max_sweeps : 16;
+  return HD_OK;
+}
+
 int hd_context_set_timing(hd_context* ctx, int enable) {
   if (!ctx) return fail(nullptr, HD_EINVAL, "hd_context_set_timing: null ctx");
   std::lock_guard<std::mutex> lk(ctx->mu);
@@ -408,7 +484,14 @@ int hd_context_reserve(hd_context* ctx, const hd_config* cfg, long nsolve) {
                                     : auto_chunk(nsolve, cfg->nstr / 2, cfg->nlyr, planck_r);
   const size_t per = hd::scratch_doubles_per_solve(cfg->nstr / 2, cfg->nlyr,
                                                    (cfg->flags & HD_FLAG_PLANCK) != 0);
-  int rc = ensure_scratch(ctx, per * std::max<long>(chunk, 1));
+  // room for hd_solve_band's epilogue too, at its largest (any nwave): so a
+  // reserved context captures either solve without growing
+  const long c1 = std::max<long>(chunk, 1);
+  const int nslot_max = hd::band_slots(1);
+  const size_t band_extra = std::max(4 * (size_t)c1 + (size_t)((c1 + 63) / 64) * nslot_max *
+                                                          2 * (size_t)(cfg->nlyr + 1),
+                                     (size_t)c1 * 2 * (size_t)(cfg->nlyr + 1));
+  int rc = ensure_scratch(ctx, per * c1 + band_extra);
   if (rc) return rc;
   rc = ensure_tables(ctx);
   if (rc) return rc;
@@ -592,7 +675,7 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
     la.nprop = cfg->nprop;
     la.nmom = nm;
     la.planck = planck;
-    la.max_sweeps = 16;
+    la.max_sweeps = ctx->max_sweeps;
     la.sink = ctx->sink;
     la.cmaj = cmaj;
     la.nwave = in->nwave;
@@ -734,7 +817,9 @@ int run_solve(hd_context* ctx, int* status, void* stream_, const char* what, Enq
   int rc = enter(ctx, stream, &capturing);
   if (rc) return rc;
   const bool sync = status == nullptr;
+  ctx->capturing = capturing;
   rc = enqueue(status, stream);
+  ctx->capturing = false;
   int any = 0;
   if (rc == HD_OK && sync) {
     const hipError_t e = hipMemcpyAsync(&any, ctx->anyerr, sizeof(int), hipMemcpyDeviceToHost, stream);
@@ -941,7 +1026,7 @@ int solve_host(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, doubl
     // the pieces' band partials, in piece (= wave) order
     double* bsum = part_d + (size_t)npiece * ncol * nlev2;
     rc = hd_band_flux(part_d, w_d + in->nwave, npiece, (int)ncol, nlev, bsum, xs);
-    if (rc) return rc;
+    if (rc) return fail(ctx, rc, "%s: band sum: %s", what, hd_last_error(nullptr));
     HD_HIP(ctx, hipEventRecord(ctx->hev_done[0], xs));
     HD_HIP(ctx, hipStreamWaitEvent(cs, ctx->hev_done[0], 0));
     HD_HIP(ctx, hipMemcpyAsync(bflux, bsum, ncol * nlev2 * sizeof(double), hipMemcpyDeviceToHost, cs));
@@ -1024,16 +1109,8 @@ int rad_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in,
   const int nm_mode = (radiances && beam) ? cfg->nstr : 1;
   const int nmom = std::max(0, std::min(cfg->nmom, cfg->nprop - 2));
 
-  rc = ensure_tables(ctx);
+  rc = ensure_rad_tables(ctx);
   if (rc) return rc;
-  if (!ctx->rad_tables) {
-    static hd::QuadHost all[hd::kMaxNN];
-    for (int q = 1; q <= hd::kMaxNN; ++q) make_quad(q, all[q - 1]);
-    hipError_t e = hd::upload_rad_tables(all);
-    if (e != hipSuccess)
-      return fail(ctx, HD_EHIP, "hd_solve_radiance: constant upload: %s", hipGetErrorString(e));
-    ctx->rad_tables = true;
-  }
   // user grid on the device: umu | phi | utau
   const size_t ngrid = (size_t)numu + nphi + rad->ntau;
   if (ngrid > ctx->rad_grid_len) {
@@ -1141,7 +1218,7 @@ int rad_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in,
     a.nprop = cfg->nprop;
     a.nmom = nmom;
     a.planck = planck;
-    a.max_sweeps = 16;
+    a.max_sweeps = ctx->max_sweeps;
     a.numu = numu;
     a.nphi = nphi;
     a.ntau = ntau;

@@ -19,6 +19,15 @@ constexpr double kPi = 3.14159265358979323846;
 // DISORT 2.0: ssalb == 1 is dithered to 1 - sqrt(10*DBL_EPSILON)
 constexpr double kDither = 4.712160915387242e-08;
 
+// harp's beam-cosine convention (legacy src/rtsolver/rt_solver_disort.cpp_:80,
+// `ds_.bc.umu0 = ray.mu > 1.E-3 ? ray.mu : 1.E-3`): umu0 is floored at 1e-3, so
+// a sun at or below the horizon is a grazing beam (fbeam > 0 still shines).
+// NaN stays NaN (the layer kernels flag it as bad input).
+constexpr double kUmu0Floor = 1.0e-3;
+__host__ __device__ __forceinline__ double umu0_floor(double mu) {
+  return mu > kUmu0Floor ? mu : (mu == mu ? kUmu0Floor : mu);
+}
+
 // per-thread status bits (mirrors include/hdisort.h)
 constexpr int kStBadInput = 0x01;
 constexpr int kStEigen = 0x02;
@@ -396,12 +405,15 @@ HD_UNROLL_NN
 // 1e-8 of its diagonal: quadratic convergence leaves ~1e-16 after it (the
 // criterion of jacobi_eig, measured one sweep earlier).  A converged lane stops
 // rotating (exact no-ops: c = 1, s = 0), so its result does not depend on which
-// solves share its wave; the loop exits when every lane has converged.
+// solves share its wave; the loop exits when every lane has converged.  Returns
+// false when this lane left at max_sweeps still rotating (not converged: the
+// caller sets the EIGEN status bit).
 template <int NN>
-__device__ __forceinline__ void jacobi_os(double (&b)[NN][NN], int max_sweeps) {
+__device__ __forceinline__ bool jacobi_os(double (&b)[NN][NN], int max_sweeps) {
+  bool on = false;
   if constexpr (NN > 1) {
     constexpr int P = NN + (NN & 1);
-    bool on = true;
+    on = true;
     for (int sweep = 0; sweep < max_sweeps; ++sweep) {
       double nrm[NN], dia = 0.0, off = 0.0;
 HD_UNROLL_NN
@@ -418,6 +430,7 @@ HD_UNROLL_NN
       if (__all(!on)) break;
     }
   }
+  return !on;
 }
 
 }  // namespace hd

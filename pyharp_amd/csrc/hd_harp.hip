@@ -12,6 +12,14 @@
 //   hd_band_optics_kernel  per (wave, col, layer, prop): tau = dz sum k c,
 //                          ssa = sum ssa k c / sum k c, moments 0
 //                          [amars_sw.cpp:261-271]
+//   hd_band_loop_kernel    per (wave, col, layer, prop): the band loop's mixing,
+//                          tau-weighted ssa, tau*ssa-weighted HG moments, +1e-10
+//                          [radiation_band.cpp:86-116]
+//
+// Floating-point contraction is off in this file's kernels: every product and
+// sum rounds as in the reference's (and the numpy restatement's) expression order,
+// so the optics are bit-identical to oracle/harp_np.py (they are bandwidth-bound,
+// the FMAs would buy nothing).
 //   hd_band_flux_kernel    per (col, level, dir): sum_w weight_w F_w in w order
 //                          [amars_lw.cpp:84-88]; hd_band_flux_wave_kernel: a
 //                          wave per output when outputs are few and bins many
@@ -24,6 +32,8 @@
 #include "../../include/hdisort.h"
 #include "hd_kernels.hpp"
 
+#pragma clang fp contract(off)
+
 namespace hd {
 namespace {
 
@@ -34,8 +44,10 @@ struct AttTables {
   const double* wl[kMaxAtt];
   const double* k[kMaxAtt];
   const double* s[kMaxAtt];
+  const double* g[kMaxAtt];  // HG asymmetry (band loop), or null
   int species[kMaxAtt];
   int natt;
+  int nv;  // values per (attenuator, wave) in coef: 2 {k, ssa} or 3 {k, ssa, g}
 };
 
 // zero-offset j with xx[j] <= x < xx[j+1] for ascending or descending xx,
@@ -55,7 +67,7 @@ __device__ int locate_dev(const double* xx, double x, int n) {
   return j - 1;
 }
 
-// coef[a][w] = {k(lambda_w), ssa(lambda_w)}
+// coef[a][w] = {k(lambda_w), ssa(lambda_w)[, g(lambda_w)]}
 __global__ __launch_bounds__(256) void hd_att_coef_kernel(AttTables T, const double* coord,
                                                           int kind, int nwave, double* coef) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -76,16 +88,20 @@ __global__ __launch_bounds__(256) void hd_att_coef_kernel(AttTables T, const dou
   const double x1 = ax[i1], x2 = ax[i2];
   const double k1 = T.k[a][i1], k2 = T.k[a][i2];
   const double s1 = T.s[a][i1], s2 = T.s[a][i2];
-  double k, s;
+  const double g1 = T.g[a] ? T.g[a][i1] : 0.0, g2 = T.g[a] ? T.g[a][i2] : 0.0;
+  double k, s, g;
   if (x2 != x1) {
     k = ((x - x1) * k2 + (x2 - x) * k1) / (x2 - x1);
     s = ((x - x1) * s2 + (x2 - x) * s1) / (x2 - x1);
+    g = ((x - x1) * g2 + (x2 - x) * g1) / (x2 - x1);
   } else {
     k = (k1 + k2) / 2.;
     s = (s1 + s2) / 2.;
+    g = (g1 + g2) / 2.;
   }
-  coef[(size_t)t * 2] = k;
-  coef[(size_t)t * 2 + 1] = s;
+  coef[(size_t)t * T.nv] = k;
+  coef[(size_t)t * T.nv + 1] = s;
+  if (T.nv > 2) coef[(size_t)t * T.nv + 2] = g;
 }
 
 __global__ __launch_bounds__(256) void hd_attenuate_kernel(const double* coef, int species,
@@ -127,6 +143,41 @@ __global__ __launch_bounds__(256) void hd_band_optics_kernel(const double* coef,
     }
     v = p == 0 ? ext * dz[cl] : (ext != 0.0 ? (sca * dz[cl]) / (ext * dz[cl]) : 0.0);
   }
+  prop[t] = v;
+}
+
+// the band loop (radiation_band.cpp:86-116), one lane per output double of
+// prop [w][c][l][2+nmom]; coef stride 3 {k, ssa, g}
+__global__ __launch_bounds__(256) void hd_band_loop_kernel(const double* coef, AttTables T,
+                                                           const double* ext0, int nwave,
+                                                           const double* conc, int ncol, int nlyr,
+                                                           int nspecies, const double* dz,
+                                                           int nprop, long n, double* prop) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int p = (int)(t % nprop);
+  const long e = t / nprop;  // (w, c, l)
+  const long cl = e % ((long)ncol * nlyr);
+  const int w = (int)(e / ((long)ncol * nlyr));
+  double ext = 0.0, sca = 0.0, mom = 0.0;
+  if (ext0) ext += ext0[e];
+  for (int a = 0; a < T.natt; ++a) {
+    const double c = conc[cl * nspecies + T.species[a]];
+    const double* cf = coef + ((size_t)a * nwave + w) * 3;
+    const double kc = cf[0] * c;
+    ext += kc;
+    sca += cf[1] * kc;
+    if (p >= 2 && T.g[a]) {  // chi_l = g^l, l = p - 1, by repeated products
+      const double g = cf[2];
+      double chi = g;
+      for (int l = 2; l < p; ++l) chi = chi * g;
+      mom += (chi * cf[1]) * kc;
+    }
+  }
+  double v;
+  if (p == 0) v = ext * dz[cl];
+  else if (p == 1) v = sca / (ext + 1e-10);
+  else v = mom / (sca + 1e-10);
   prop[t] = v;
 }
 
@@ -191,8 +242,10 @@ unsigned nblk(long n, int b) { return (unsigned)((n + b - 1) / b); }
 int pack_tables(const hd_attenuator* atts, int natt, AttTables& T) {
   if (natt < 1 || natt > kMaxAtt) return set_global_error(HD_EINVAL, "natt=%d not in [1, %d]", natt, kMaxAtt);
   T.natt = natt;
+  T.nv = 2;
   for (int a = 0; a < natt; ++a) {
     const hd_attenuator& at = atts[a];
+    T.g[a] = nullptr;
     if (at.nrow < 1 || !at.wavelength || !at.kext || !at.ssa || at.species < 0)
       return set_global_error(HD_EINVAL, "attenuator %d: bad table (nrow=%d species=%d)", a,
                               at.nrow, at.species);
@@ -335,6 +388,49 @@ int hd_band_optics(const hd_attenuator* atts, int natt, const double* coord, int
   hipLaunchKernelGGL(hd::hd_band_optics_kernel, dim3(nblk(n, 256)), dim3(256), 0, s, coef, T,
                      nwave, conc, ncol, nlyr, nspecies, dz, nprop, n, prop);
   rc = hd::launched("hd_band_optics");
+  (void)hipFreeAsync(coef, s);
+  return rc;
+}
+
+int hd_band_loop_optics(const hd_band_attenuator* atts, int natt, const double* ext0,
+                        const double* coord, int coord_kind, int nwave, const double* conc,
+                        int ncol, int nlyr, int nspecies, const double* dz, int nmom,
+                        double* prop, void* stream_) {
+  if (!atts || nwave < 0 || ncol < 0 || nlyr < 0 || nspecies < 1 || nmom < 0 ||
+      (coord_kind != HD_COORD_WAVELENGTH && coord_kind != HD_COORD_WAVENUMBER))
+    return hd::set_global_error(HD_EINVAL, "hd_band_loop_optics: bad arguments");
+  if (natt < 1 || natt > hd::kMaxAtt)
+    return hd::set_global_error(HD_EINVAL, "hd_band_loop_optics: natt=%d not in [1, %d]", natt,
+                                hd::kMaxAtt);
+  hd_attenuator tabs[hd::kMaxAtt];
+  for (int a = 0; a < natt; ++a) tabs[a] = atts[a].table;
+  hd::AttTables T{};
+  int rc = hd::pack_tables(tabs, natt, T);
+  if (rc) return rc;
+  T.nv = 3;
+  for (int a = 0; a < natt; ++a) {
+    if (atts[a].table.species >= nspecies)
+      return hd::set_global_error(HD_EINVAL,
+                                  "hd_band_loop_optics: attenuator %d species %d >= %d", a,
+                                  atts[a].table.species, nspecies);
+    T.g[a] = atts[a].gasym;
+  }
+  const int nprop = 2 + nmom;
+  const long n = (long)nwave * ncol * nlyr * nprop;
+  if (n == 0) return HD_OK;
+  if (!coord || !conc || !dz || !prop)
+    return hd::set_global_error(HD_EINVAL, "hd_band_loop_optics: null array");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream_);
+  double* coef = nullptr;
+  if (hipMallocAsync((void**)&coef, (size_t)natt * nwave * 3 * sizeof(double), s) != hipSuccess) {
+    (void)hipGetLastError();
+    return hd::set_global_error(HD_ENOMEM, "hd_band_loop_optics: scratch allocation failed");
+  }
+  hipLaunchKernelGGL(hd::hd_att_coef_kernel, dim3(nblk((long)natt * nwave, 256)), dim3(256), 0,
+                     s, T, coord, coord_kind, nwave, coef);
+  hipLaunchKernelGGL(hd::hd_band_loop_kernel, dim3(nblk(n, 256)), dim3(256), 0, s, coef, T, ext0,
+                     nwave, conc, ncol, nlyr, nspecies, dz, nprop, n, prop);
+  rc = hd::launched("hd_band_loop_optics");
   (void)hipFreeAsync(coef, s);
   return rc;
 }

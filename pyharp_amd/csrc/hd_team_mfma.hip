@@ -213,10 +213,10 @@ __global__ __launch_bounds__(64, 2) void hd_team_mfma_layer_kernel(LayerArgs A) 
   const double om = ssa * (1.0 - f) / (1.0 - ssa * f);
   const double rf = om / (1.0 - f);
 
-  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
+  const double mu0 = A.umu0 ? umu0_floor(A.umu0[s]) : 1.0;
   const double fb = A.fbeam ? A.fbeam[s] : 0.0;
   const bool beam = fb > 0.0 && mu0 > 0.0;
-  if (beam && mu0 > 1.0) st |= kStBadInput;
+  if (fb > 0.0 && !(mu0 <= 1.0)) st |= kStBadInput;
   const double rmu0 = beam ? 1.0 / mu0 : 0.0;
   const double mub = beam ? mu0 : 0.0;
 
@@ -315,7 +315,7 @@ __global__ __launch_bounds__(64, 2) void hd_team_mfma_layer_kernel(LayerArgs A) 
 
   // ---- eigenpairs (c_soleig): Sym = L^T S+ L = B0^T B0 = V diag(k^2) V^T ----
   lds_fence();
-  team_jacobi<NN>(bcol, A.max_sweeps);  // B = B0 V, lane j: column j
+  if (!team_jacobi<NN>(bcol, A.max_sweeps)) st |= kStEigen;  // B = B0 V, lane j: column j
   lds_fence();
   double kk;
   {
@@ -511,7 +511,7 @@ __global__ __launch_bounds__(64, 1) void hd_team_mfma_sweep_kernel(SweepArgs A) 
   for (int k = lane; k < 2 * kSet; k += 64) lds[k] = 0.0;
   lds_fence();
 
-  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
+  const double mu0 = A.umu0 ? umu0_floor(A.umu0[s]) : 1.0;
   const double fb = A.fbeam ? A.fbeam[s] : 0.0;
   const bool beam = fb > 0.0 && mu0 > 0.0;
   const double alb = A.albedo ? A.albedo[s] : 0.0;

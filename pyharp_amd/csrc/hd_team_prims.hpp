@@ -287,9 +287,10 @@ __device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double& own, 
 
 // Sweeps of rounds 1..15 until the sweep that was the last one needed
 // (kJacobiLastFrob2), or max_sweeps.  A converged team issues no-op rotations
-// (c = 1, s = 0) while its wave-mates finish.
+// (c = 1, s = 0) while its wave-mates finish.  Returns false when the team left
+// at max_sweeps with pairs still rotating (the caller sets the EIGEN status bit).
 template <int NN>
-__device__ __forceinline__ void team_jacobi(double (&b)[NN], int max_sweeps) {
+__device__ __forceinline__ bool team_jacobi(double (&b)[NN], int max_sweeps) {
   bool on = true;
   double sig = 1.0;  // b = sig x (HD_JACOBI_SCALED)
   for (int sweep = 0; sweep < max_sweeps; ++sweep) {
@@ -310,6 +311,7 @@ __device__ __forceinline__ void team_jacobi(double (&b)[NN], int max_sweeps) {
     if (__all(!on)) break;
   }
   sfor<0, NN>([&](auto K) { b[HD_K(K)] *= sig; });
+  return !on;
 }
 
 }  // namespace team

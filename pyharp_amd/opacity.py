@@ -13,7 +13,11 @@ Mirrors the two attenuators pyharp's SW example builds its optics from
   linearly in wavelength and clamped at the table ends (interpn.h, locate.h);
 * ``band_optics`` -- the assembly amars_sw.cpp:261-271 performs by hand
   (sum of attenuators, x dz, ssa = sum ssa k c / sum k c), fused into one
-  kernel that writes the solver's prop layout directly.
+  kernel that writes the solver's prop layout directly (SURVEY 8(f) rank 1);
+* ``band_loop_optics`` -- the library band loop's mixing
+  (src/radiation/radiation_band.cpp:86-116: tau-weighted ssa, tau*ssa-weighted
+  phase moments, the +1e-10 regularisation), with Henyey-Greenstein moments
+  from an attenuator's asymmetry table (``set_asymmetry``), into the same layout.
 
 The arithmetic runs in libhdisort.so (include/hdharp.h); tables are read on
 the host (file parsing is not on the device path).  There is no CPU compute
@@ -157,17 +161,30 @@ class _TableAttenuator:
         self.kwave = torch.as_tensor(t[:, 0].copy())              # [um]
         self.kdata = torch.as_tensor(t[:, 1:].copy())             # (rows, 2)
         self.kdata[:, 0] *= w[sid]                                # m^2/kg -> m^2/mol
+        self.gasym = None                                         # HG asymmetry per row
         self._dev_tables = {}
+
+    def set_asymmetry(self, g) -> "_TableAttenuator":
+        """Henyey-Greenstein asymmetry g(lambda) per table row (scalar: every row),
+        the phase moments chi_l = g^l this attenuator brings to band_loop_optics
+        (the reference's tables carry none: data/*.txt hold k_ext and ssa only)."""
+        g = np.broadcast_to(np.asarray(g, np.float64), (self.kwave.numel(),)).copy()
+        if not np.all(np.abs(g) < 1.0):
+            raise RuntimeError("set_asymmetry: |g| must be < 1")
+        self.gasym = torch.as_tensor(g)
+        self._dev_tables = {}
+        return self
 
     def _tables(self, dev):
         key = str(dev)
         if key not in self._dev_tables:
             self._dev_tables[key] = (_f64(self.kwave, dev), _f64(self.kdata[:, 0], dev),
-                                     _f64(self.kdata[:, 1], dev))
+                                     _f64(self.kdata[:, 1], dev),
+                                     None if self.gasym is None else _f64(self.gasym, dev))
         return self._dev_tables[key]
 
     def hd_struct(self, dev) -> _lib.HdAttenuator:
-        wl, k, s = self._tables(dev)
+        wl, k, s, _ = self._tables(dev)
         return _lib.HdAttenuator(nrow=int(wl.numel()), wavelength=wl.data_ptr(),
                                  kext=k.data_ptr(), ssa=s.data_ptr(),
                                  species=int(self.options.species_ids()[0]))
@@ -229,6 +246,50 @@ def band_optics(attenuators: Sequence[_TableAttenuator], conc: torch.Tensor, dz:
         _lib.check(lib.hd_band_optics(atts, len(attenuators), x.data_ptr(), kind, nwave,
                                       c.data_ptr(), ncol, nlyr, nsp, d.data_ptr(), nprop,
                                       out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream))
+    return out
+
+
+def band_loop_optics(attenuators: Sequence[_TableAttenuator], conc: torch.Tensor,
+                     dz: torch.Tensor, kwargs: Dict[str, torch.Tensor], nmom: int,
+                     ext0: Optional[torch.Tensor] = None,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """prop (nwave, ncol, nlyr, 2 + nmom) by RadiationBandImpl::forward's mixing
+    (src/radiation/radiation_band.cpp:86-116), on the device (hd_band_loop_optics):
+    ext = ext0 + sum_a k_a c_a, ssa = sum_a ssa_a k_a c_a / (ext + 1e-10), moments
+    sum_a g_a^l ssa_a k_a c_a / (sum_a ssa_a k_a c_a + 1e-10) over the attenuators
+    with an asymmetry table, tau = ext dz -- in the reference's operation order.
+    ext0: (nwave, ncol, nlyr[, 1]) extinction of attenuators without ssa (an RFM
+    module's forward), added first."""
+    coord, kind = _coord(kwargs)
+    dev = _device(conc, coord, dz)
+    c = _f64(conc, dev)
+    ncol, nlyr, nsp = c.shape
+    d = torch.as_tensor(dz, dtype=torch.float64)
+    if d.dim() == 2 and d.shape == (nlyr, 1):
+        d = d[:, 0]
+    d = _f64(d.expand(ncol, nlyr), dev)
+    x = _f64(coord, dev).reshape(-1)
+    nwave = x.numel()
+    e0 = None
+    if ext0 is not None:
+        e0 = _f64(ext0, dev)
+        if e0.numel() != nwave * ncol * nlyr:
+            raise RuntimeError(f"band_loop_optics: ext0 must hold {(nwave, ncol, nlyr)}")
+    if out is None:
+        out = torch.empty((nwave, ncol, nlyr, 2 + nmom), dtype=torch.float64, device=dev)
+    structs = []
+    for a in attenuators:
+        g = a._tables(dev)[3]
+        structs.append(_lib.HdBandAttenuator(table=a.hd_struct(dev),
+                                             gasym=None if g is None else g.data_ptr()))
+    atts = (_lib.HdBandAttenuator * len(structs))(*structs)
+    lib = _lib.load()
+    with torch.cuda.device(dev):
+        _lib.check(lib.hd_band_loop_optics(atts, len(structs),
+                                           None if e0 is None else e0.data_ptr(), x.data_ptr(),
+                                           kind, nwave, c.data_ptr(), ncol, nlyr, nsp,
+                                           d.data_ptr(), int(nmom), out.data_ptr(),
+                                           torch.cuda.current_stream(dev).cuda_stream))
     return out
 
 

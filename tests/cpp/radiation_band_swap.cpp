@@ -11,7 +11,7 @@
 // Two bands run on two host threads at once (SURVEY 8(b) "Threading": one
 // hd_context per (device, host thread)), each three times; the last result
 // of each is printed as "band w c l up dn" and checked against the oracle by
-// tests/test_gpu_parity.py::test_cpp_radiation_band_swap.
+// tests/test_gpu_concurrency.py::test_cpp_radiation_band_swap.
 #include <harp_amd/disort.hpp>
 
 #include <cmath>
@@ -93,7 +93,7 @@ struct Band {
 }  // namespace pyharp_side
 
 // band 0: SW beam, nstr 8, HG moments; band 1: LW planck, nstr 4, omega = 0
-// (tests/test_gpu_parity.py::_swap_inputs restates these formulas)
+// (tests/test_gpu_concurrency.py::_swap_inputs restates these formulas)
 static void inputs(int band, int nwave, int ncol, int nlyr, int nstr, torch::Tensor& prop,
                    std::map<std::string, torch::Tensor>& bc, torch::Tensor& temf) {
   const int nprop = 2 + nstr;

@@ -264,3 +264,32 @@ def test_cpp_amars_lw(oracle_c, tmp_path):
                             wave_lower=np.full(nw, 1.0), wave_upper=np.full(nw, 150.0))
     bref = H.band_flux(fref, fx["weights"])
     assert rel_err(bflx[None], bref).max() < TOL
+
+
+@pytest.mark.parametrize("nmom", [0, 8, 32])
+@pytest.mark.parametrize("rfm", [False, True])
+def test_band_loop_optics_bit_identical(nmom, rfm):
+    """hd_band_loop_optics (radiation_band.cpp:86-116 on the device) equals the numpy
+    restatement bit for bit on the reference's data tables (which
+    tests/test_harp_oracle.py pins to the reference's statement order): s8 with a
+    wavelength-dependent HG asymmetry, h2so4 with a constant one; wavenumbers inside,
+    at and beyond the table ends; an RFM-like extinction added first."""
+    from pyharp_amd.opacity import band_loop_optics
+    s8, h2 = _attenuators()
+    tabs = _oracle_tables()
+    g8 = np.linspace(0.6, 0.85, s8.kwave.numel())
+    s8.set_asymmetry(g8)
+    h2.set_asymmetry(0.75)
+    otabs = [(tabs[0][0], tabs[0][1], 0, g8), (tabs[1][0], tabs[1][1], 1, H.hg_table(tabs[1][0], 0.75))]
+    rng = np.random.default_rng(31 + nmom)
+    ncol, nlyr = 4, 9
+    conc = rng.uniform(0, 1e-5, (ncol, nlyr, 2))
+    conc[1, 2] = 0.0
+    dz = rng.uniform(100, 2000, (ncol, nlyr))
+    wave = np.r_[np.linspace(2000.0, 50000.0, 37), 1e4 / tabs[0][0][0], 100.0, 1e6]
+    ext0 = rng.uniform(0, 1e-3, (wave.size, ncol, nlyr)) if rfm else None
+    got = band_loop_optics([s8, h2], torch.as_tensor(conc, device=DEV), torch.as_tensor(dz),
+                           {"wavenumber": torch.as_tensor(wave, device=DEV)}, nmom,
+                           ext0=None if ext0 is None else torch.as_tensor(ext0, device=DEV))
+    ref = H.band_loop_optics(otabs, conc, dz, nmom, wavenumber=wave, ext0=ext0)
+    np.testing.assert_array_equal(got.cpu().numpy(), ref)

@@ -515,3 +515,115 @@ def test_full_c4_size_properties(oracle_c):
         oracle_c.forward(pn, bn, nstr=nstr, first=int(q), count=1, out=ref)
     got = f.cpu().numpy().reshape(-1, L + 1, 2)[idx]
     assert rel_err(got, ref.reshape(-1, L + 1, 2)[idx]).max() < TOL
+
+
+@pytest.mark.parametrize("nstr", [8, 32])
+def test_umu0_floor(oracle_c, nstr):
+    """harp's beam cosine floor, ``umu0 = mu > 1e-3 ? mu : 1e-3`` (legacy
+    /root/reference/src/rtsolver/rt_solver_disort.cpp_:80):
+    umu0 in {-0.5, 0, 1e-4, 1e-3, 2e-3} on the register (nstr 8) and team (nstr 32)
+    kernels against the C oracle, which applies the same floor; the first three
+    equal the 1e-3 solve bit for bit."""
+    rng = np.random.default_rng(4242 + nstr)
+    u = np.array([-0.5, 0.0, 1e-4, 1e-3, 2e-3])
+    nwave, ncol, nlyr = 2, u.size, 20
+    prop, bc, _ = _random_batch(rng, nwave, ncol, nlyr, nstr, False)
+    prop[..., 0] = 10.0 ** rng.uniform(-5, -1.5, (nwave, ncol, nlyr))  # the grazing beam survives
+    bc["umu0"] = np.broadcast_to(u, (nwave, ncol)).copy()
+    ref = oracle_c.forward(prop, bc, nstr=nstr)
+    d = _disort(nstr, nlyr, nwave, ncol)
+    f = _run(d, prop, bc)
+    err = rel_err(f, ref).max()
+    assert err < TOL, f"nstr={nstr}: max rel err {err:.3e}"
+    g = _run(d, prop, dict(bc, umu0=np.full((nwave, ncol), 1e-3)))
+    np.testing.assert_array_equal(f[:, :3], g[:, :3])
+    assert np.all(f[:, :, -1, 1] > 0.0)  # the floored beam shines at the top
+
+
+@pytest.mark.parametrize("nstr", [8, 32])
+def test_eigen_status_when_jacobi_capped(nstr):
+    """A Jacobi still rotating at the sweep cap is reported (HD_STATUS_EIGEN, an
+    error bit: the synchronous call raises) -- on the register (nstr 8) and team
+    (nstr 32) layer kernels; with the default cap the same inputs are clean."""
+    from pyharp_amd import _lib
+    from pyharp_amd.disort import _context
+    rng = np.random.default_rng(99 + nstr)
+    nwave, ncol, nlyr = 2, 40, 10
+    prop, bc, _ = _random_batch(rng, nwave, ncol, nlyr, nstr, False)
+    d = _disort(nstr, nlyr, nwave, ncol)
+    dev = torch.device("cuda", 0)
+    st = torch.zeros(nwave * ncol, dtype=torch.int32, device=dev)
+    ctx = _context(0)
+    try:
+        ctx.set_max_sweeps(1)
+        _run(d, prop, bc, status=st)
+        torch.cuda.synchronize()
+        eig = (st & _lib.HD_STATUS_EIGEN) != 0
+        assert int(eig.sum()) > nwave * ncol // 2, int(eig.sum())
+        with pytest.raises(RuntimeError, match="numerical failure"):
+            _run(d, prop, bc)
+    finally:
+        ctx.set_max_sweeps(0)
+    _run(d, prop, bc, status=st)
+    torch.cuda.synchronize()
+    assert int((st & _lib.HD_STATUS_ERROR_MASK).sum()) == 0
+
+
+@pytest.mark.parametrize("nstr", [8, 32])
+def test_reserve_then_capture_band(nstr):
+    """hd_context_reserve sizes hd_solve_band's epilogue too: on a fresh context
+    (a new host thread's), capturing the fused band solve without a reserve is
+    refused with HD_EINVAL (no free/malloc inside the capture), and after a
+    reserve the captured solve replays to the eager result bit for bit."""
+    import threading
+    from pyharp_amd import _lib
+    from pyharp_amd.disort import _context
+    rng = np.random.default_rng(60 + nstr)
+    nwave, ncol, nlyr = 5, 30, 12
+    prop, bc, _ = _random_batch(rng, nwave, ncol, nlyr, nstr, False)
+    dev = torch.device("cuda", 0)
+    p = torch.as_tensor(prop, device=dev)
+    b = {k: torch.as_tensor(v, device=dev) for k, v in bc.items()}
+    w = torch.as_tensor(rng.uniform(0.1, 1.0, nwave), device=dev)
+    res = {}
+
+    def worker():
+        try:
+            d = _disort(nstr, nlyr, nwave, ncol)
+            st = torch.zeros(nwave * ncol, dtype=torch.int32, device=dev)
+            out = torch.empty((ncol, nlyr + 1, 2), dtype=torch.float64, device=dev)
+            s = torch.cuda.Stream(device=dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            g0 = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.stream(s):
+                    with torch.cuda.graph(g0, stream=s):
+                        d.forward_band(p, b, weights=w, out=out, status=st)
+            except RuntimeError as e:
+                res["refused"] = str(e)
+            torch.cuda.synchronize()
+            cfg = _lib.HdConfig(nstr=nstr, nmom=nstr, nlyr=nlyr, nprop=prop.shape[-1],
+                                flags=_lib.HD_FLAG_LAMBER | _lib.HD_FLAG_ONLYFL)
+            _context(0).reserve(cfg, nwave * ncol)
+            g = torch.cuda.CUDAGraph()
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s):
+                    d.forward_band(p, b, weights=w, out=out, status=st)
+            out.zero_()
+            g.replay()
+            torch.cuda.synchronize()
+            res["replay"] = out.clone()
+            res["eager"] = d.forward_band(p, b, weights=w)
+            torch.cuda.synchronize()
+        except BaseException as e:  # surfaced in the main thread
+            res["error"] = e
+
+    t = threading.Thread(target=worker)
+    t.start()
+    t.join(timeout=100)
+    assert not t.is_alive()
+    if "error" in res:
+        raise res["error"]
+    assert "inside a stream capture" in res.get("refused", ""), res.get("refused")
+    assert torch.equal(res["replay"], res["eager"])

@@ -314,3 +314,25 @@ def test_ims_aureole_vs_oracle(nstr, monkeypatch):
     _, utms = disort_rad_forward(prop, bc, nstr=nstr, nmom=nmom, umu=umu, phi=phi, utau=utau,
                                  corint=True)
     assert _col_err(uref, utms) > 1e-4   # the IMS term is resolved by the comparison
+
+
+def test_radiance_umu0_floor():
+    """The intensity path applies harp's umu0 floor (rt_solver_disort.cpp_:80) like
+    the flux path: umu0 in {0, 1e-4, 1e-3, 2e-3} against the radiance oracle."""
+    rng = np.random.default_rng(5150)
+    nwave, ncol, nlyr, nstr = 1, 4, 4, 8
+    prop, bc, _ = _random_case(rng, nwave, ncol, nlyr, nstr, False)
+    prop[..., 0] = 10.0 ** rng.uniform(-4, -2, (nwave, ncol, nlyr))
+    bc["umu0"] = np.array([[0.0, 1e-4, 1e-3, 2e-3]])
+    total = prop[..., 0].sum(axis=-1).min()
+    utau = [0.0, 0.5 * total, total]
+    umu = [-1.0, -0.3, 0.2, 0.9]
+    phi = [0.0, 120.0]
+    d = _disort(nstr, nlyr, nwave, ncol, flags="usrtau,usrang,lamber,quiet", umu=umu, phi=phi,
+                utau=utau)
+    flux = d.forward(torch.as_tensor(prop, device=DEV), _dev(bc)).cpu().numpy()
+    uu = d.get_rad().cpu().numpy()
+    fref, uref = disort_rad_forward(prop, bc, None, nstr=nstr, umu=umu, phi=phi, utau=utau)
+    assert _col_err(uu, uref) < TOL, _col_err(uu, uref)
+    assert rel_err(flux, fref).max() < TOL
+    np.testing.assert_array_equal(uu[0, 0], uu[0, 2])

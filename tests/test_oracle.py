@@ -139,3 +139,27 @@ def test_layer2level_matches_reference_run():
     out = disort_np.layer2level([300.0, 280.0, 260.0, 250.0, 240.0])
     np.testing.assert_allclose(out, [310.0, 290.0, 269.1666666667, 254.1666666667, 245.0, 240.0],
                                rtol=1e-10)
+
+
+@pytest.mark.parametrize("nstr", [8, 32])
+def test_umu0_floor_in_both_oracles(nstr, oracle_c):
+    """harp's beam cosine floor (legacy src/rtsolver/rt_solver_disort.cpp_:80,
+    ``umu0 = mu > 1e-3 ? mu : 1e-3``): umu0 in {-0.4, 0, 1e-4} solves as 1e-3 in
+    both restatements' batch drivers, 2e-3 does not, and numpy == C."""
+    rng = np.random.default_rng(77 + nstr)
+    nlyr = 6
+    u = np.array([[-0.4, 0.0, 1e-4, 1e-3, 2e-3]])
+    prop = np.zeros((1, u.shape[1], nlyr, 2 + nstr))
+    prop[..., 0] = 10.0 ** rng.uniform(-4, -1, (nlyr,))  # thin: the grazing beam survives
+    prop[..., 1] = rng.uniform(0.2, 0.95, (nlyr,))
+    g = rng.uniform(0.1, 0.8, (nlyr,))
+    for l in range(nstr):
+        prop[..., 2 + l] = g ** (l + 1)
+    bc = {"fbeam": np.ones_like(u), "umu0": u, "albedo": np.full_like(u, 0.3)}
+    fc = oracle_c.forward(prop, bc, nstr=nstr)
+    fn = disort_np.disort_forward(prop, bc, nstr=nstr)
+    assert rel_err(fn, fc).max() < 1e-9
+    for j in range(3):
+        np.testing.assert_array_equal(fc[0, j], fc[0, 3])
+    assert np.abs(fc[0, 4] - fc[0, 3]).max() > 1e-6 * np.abs(fc[0, 3]).max()
+    assert fc[0, 3, -1, 1] > 0.0  # the floored beam still shines at the top
