@@ -1,9 +1,10 @@
-"""Fold rocprofv3 FETCH_SIZE / WRITE_SIZE passes into profiles/pmc_latest.json.
+"""Fold rocprofv3 FETCH_SIZE / WRITE_SIZE passes into profiles/pmc_<shape>.json (read by bench.py).
 
-    python scripts/pmc_summarize.py gpurun_out/TAG [--solves 65536] [--nstr 16] [--nlyr 80]
+    python scripts/pmc_summarize.py FETCH_DIR WRITE_DIR [--solves 65536] [--nstr 16] [--nlyr 80]
+                                    [--out profiles/pmc_c4.json]
 
-Inputs are the two separate `--pmc` passes written by scripts/gpu_check.sh over
-scripts/pmc_run.py (one 65 536-solve chunk of the C4 shape per launch).  Units:
+Inputs are the two separate `--pmc` passes (scripts/gpu.sh step pmc=NAME:NSTR) over
+scripts/pmc_run.py (one chunk of the C4 or C5 shape per launch).  Units:
 rocprofv3 reports both counters in KiB.  gfx950 correction
 (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts half the bytes of a wide
 coalesced streaming read, so fetch is doubled; WRITE_SIZE is exact.  Our
@@ -14,12 +15,15 @@ bytes (layer records + back-substitution records) match 2 x FETCH_SIZE to 2 %.
 
 import argparse
 import csv
+import glob
 import json
 import os
 
 
-def per_kernel(path, counter):
+def per_kernel(run_dir, counter):
     acc = {}
+    path = sorted(glob.glob(os.path.join(run_dir, "**", "*counter_collection.csv"),
+                            recursive=True))[0]
     with open(path) as f:
         for r in csv.DictReader(f):
             if r["Counter_Name"] != counter:
@@ -34,18 +38,17 @@ def per_kernel(path, counter):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("run_dir")
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
     ap.add_argument("--solves", type=int, default=65536)
     ap.add_argument("--nstr", type=int, default=16)
     ap.add_argument("--nlyr", type=int, default=80)
     ap.add_argument("--planck", action="store_true")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles",
-                                                   "pmc_latest.json"))
+                                                   "pmc_c4.json"))
     a = ap.parse_args()
-    fetch = per_kernel(os.path.join(a.run_dir, "pmc_fetch", "pmc_counter_collection.csv"),
-                       "FETCH_SIZE")
-    write = per_kernel(os.path.join(a.run_dir, "pmc_write", "pmc_counter_collection.csv"),
-                       "WRITE_SIZE")
+    fetch = per_kernel(a.fetch_dir, "FETCH_SIZE")
+    write = per_kernel(a.write_dir, "WRITE_SIZE")
     kernels = {}
     for k in sorted(set(fetch) | set(write)):
         rd = 2.0 * fetch.get(k, 0.0)
@@ -53,7 +56,7 @@ def main():
         kernels[k] = {"fetch_bytes_raw": fetch.get(k), "read_bytes": rd, "write_bytes": wr,
                       "bytes_per_launch": rd + wr, "bytes_per_solve": (rd + wr) / a.solves}
     out = {"nstr": a.nstr, "nlyr": a.nlyr, "planck": bool(a.planck),
-           "solves_per_launch": a.solves, "source": os.path.basename(os.path.normpath(a.run_dir)),
+           "solves_per_launch": a.solves, "source": os.path.normpath(a.fetch_dir).replace("_fetch", ""),
            "correction": "read = 2 x FETCH_SIZE (gfx950 half-count), write = WRITE_SIZE; KiB -> B",
            "kernels": kernels}
     with open(a.out, "w") as f:

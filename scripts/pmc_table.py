@@ -1,6 +1,6 @@
 """Per-kernel averages of every counter in a pmc run directory (one or more passes).
 
-    python scripts/pmc_table.py gpurun_out/TAG [--json out.json]
+    python scripts/pmc_table.py DIR [DIR ...] [--json out.json]   (every *counter_collection.csv below)
 """
 import argparse
 import csv
@@ -11,11 +11,13 @@ import os
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("run_dir")
+    ap.add_argument("run_dirs", nargs="+")
     ap.add_argument("--json")
     a = ap.parse_args()
     acc = {}
-    for path in sorted(glob.glob(os.path.join(a.run_dir, "*", "pmc_counter_collection.csv"))):
+    paths = [p for d in a.run_dirs
+             for p in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)]
+    for path in sorted(paths):
         with open(path) as f:
             for r in csv.DictReader(f):
                 name = r["Kernel_Name"]

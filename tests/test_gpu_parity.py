@@ -589,6 +589,7 @@ def test_reserve_then_capture_band(nstr):
 
     def worker():
         try:
+            _context(0)  # this thread's fresh context: created outside the capture
             d = _disort(nstr, nlyr, nwave, ncol)
             st = torch.zeros(nwave * ncol, dtype=torch.int32, device=dev)
             out = torch.empty((ncol, nlyr + 1, 2), dtype=torch.float64, device=dev)
