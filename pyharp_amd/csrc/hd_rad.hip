@@ -1563,8 +1563,11 @@ static void launch_rad(const RadArgs& a, bool radiances, hipStream_t st) {
   const unsigned nb1 = (unsigned)(((a.nu + 63) / 64) *
                                   ((a.nlyr + kLayersPerBlockR - 1) / kLayersPerBlockR));
   hipLaunchKernelGGL(hd_rad_layer_kernel<NN>, dim3(nb1), dim3(kLayerBlockR), 0, st, a);
-  hipLaunchKernelGGL(hd_rad_sweep_kernel<NN>, dim3((unsigned)((a.nu + 63) / 64)), dim3(64), 0, st,
-                     a);
+  if constexpr (NN > kMaxRegNN)
+    (void)hd::launch_rad_team_sweep(NN, a, st);  // team layout + MFMA (hd_team_mfma.hip)
+  else
+    hipLaunchKernelGGL(hd_rad_sweep_kernel<NN>, dim3((unsigned)((a.nu + 63) / 64)), dim3(64), 0,
+                       st, a);
   const long nc = (long)a.nu * a.nlyr;
   hipLaunchKernelGGL(hd_rad_const_kernel<NN>, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0,
                      st, a);

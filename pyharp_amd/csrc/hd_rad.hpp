@@ -76,6 +76,9 @@ hipError_t upload_rad_tables(const QuadHost* per_nn);  // nn 1..kRadMaxNN
 // radiances = false: fluxes at the user depths only (mode 0, no uu)
 hipError_t launch_rad_chunk(int nn, const RadArgs& a, bool radiances, hipStream_t stream);
 size_t rad_scratch_doubles_per_unit(int nn, int nlyr);
+// nstr 18..32: the adding sweep + back-substitution on the team layout with the
+// dense products on FP64 MFMA, four units per wave (hd_team_mfma.hip)
+hipError_t launch_rad_team_sweep(int nn, const RadArgs& a, hipStream_t stream);
 // nstr 18..32: the same kernels compiled with rolled NN-loops (hd_rad_wide.hip)
 namespace wide {
 hipError_t upload_rad_tables(const QuadHost* per_nn);

@@ -32,6 +32,7 @@
 // Replaces the DPP-broadcast products of hd_team_layer_kernel, whose row
 // broadcasts, 64-bit selects and register spills were 39% of its VALU
 // instructions at one wave per SIMD (profiles/r02_c5_team_counters_v1.json).
+#include "hd_rad.hpp"
 #include "hd_team_prims.hpp"
 
 namespace hd {
@@ -624,24 +625,35 @@ __global__ __launch_bounds__(64, 1) void hd_team_mfma_sweep_kernel(SweepArgs A) 
     double u = sd;
     sfor<0, NN>([&](auto K) { u = fma(ra[HD_K(K)], bc<HD_K(K)>(t1), u); });
     bw[NN * NN + ii] = t1;
-    // ZT = W1^-1 T (row-sequential solves) -> record, and to M layout through LDS
-    double zt[NN];
-    sfor<0, NN>([&](auto J) { zt[HD_K(J)] = tr[HD_K(J)]; });
-    sfor<0, NN>([&](auto K) {
-      constexpr int k = HD_K(K);
-      const double mm = i > k ? w[k] : 0.0;
-      sfor<0, NN>([&](auto J) { zt[HD_K(J)] = fma(-mm, bc<k>(zt[HD_K(J)]), zt[HD_K(J)]); });
-    });
-    sfor_rev<0, NN>([&](auto K) {
-      constexpr int k = HD_K(K);
-      const double sc = i == k ? w[k] : 1.0;
-      sfor<0, NN>([&](auto J) { zt[HD_K(J)] *= sc; });
-      const double mm = i < k ? w[k] : 0.0;
-      sfor<0, NN>([&](auto J) { zt[HD_K(J)] = fma(-mm, bc<k>(zt[HD_K(J)]), zt[HD_K(J)]); });
-    });
-    sfor<0, NN>([&](auto J) { bw[ii * NN + HD_K(J)] = zt[HD_K(J)]; });
-    sfor<0, NN>([&](auto J) { zt[HD_K(J)] *= msk; });
-    put_rows<NN>(S1, t, i, zt);
+    // ZT = W1^-1 T = U^-1 (L^-1 T) on the matrix core: the team forms the columns
+    // of L^-1 (unit lower) and U^-1 from the LU rows -- lane i holds column i, i.e.
+    // row i of the transposed inverse, the operand the M-layout product wants --
+    // instead of sixteen row-sequential triangular solves with T's sixteen columns
+    // (NN(NN-1) broadcasts per lane against 2 x NN(NN-1)/2 here)
+    {
+      double zl[NN], zu[NN];
+      sfor<0, NN>([&](auto R) {  // column i of L^-1: z_r = delta_ri - sum_{k<r} L_rk z_k
+        constexpr int r = HD_K(R);
+        double v = i == r ? 1.0 : 0.0;
+        sfor<0, r>([&](auto K) { v = fma(-bc<r>(w[HD_K(K)]), zl[HD_K(K)], v); });
+        zl[r] = v;
+        pin<NN>(w);
+      });
+      sfor_rev<0, NN>([&](auto R) {  // column i of U^-1: z_r = (delta_ri - sum_{k>r} U_rk z_k) / U_rr
+        constexpr int r = HD_K(R);
+        double v = i == r ? 1.0 : 0.0;
+        sfor<r + 1, NN>([&](auto K) { v = fma(-bc<r>(w[HD_K(K)]), zu[HD_K(K)], v); });
+        zu[r] = v * bc<r>(w[r]);  // reciprocal pivot on the diagonal
+        pin<NN>(w);
+      });
+      sfor<0, NN>([&](auto J) {
+        zl[HD_K(J)] *= msk;
+        zu[HD_K(J)] *= msk;
+      });
+      lds_fence();
+      put_rows<NN>(S0, t, i, zl);  // L^-T, row-major
+      put_rows<NN>(S1, t, i, zu);  // U^-T, row-major
+    }
     // Sd <- T u + S-
     {
       double tq = sml;
@@ -649,10 +661,24 @@ __global__ __launch_bounds__(64, 1) void hd_team_mfma_sweep_kernel(SweepArgs A) 
       sd = tq * msk;
     }
     lds_fence();
-    // A <- R + T (A ZT) on the matrix core; then A's rows to the team layout
+    // ZT = U^-1 (L^-1 T); record (M layout: rows h + 4m, column c); A <- R + T (A ZT);
+    // then A's rows to the team layout
     {
-      double zm[4][4], pm[4][4];
-      get_m(S1, h, c, zm);
+      double li[4][4], x1[4][4], zm[4][4], pm[4][4];
+      get_m(S0, h, c, li);
+      mprod<false>(li, tm, x1, h, c);  // L^-1 T
+      get_m(S1, h, c, li);
+      mprod<false>(li, x1, zm, h, c);  // ZT = U^-1 (L^-1 T)
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        double* zr = A.bsub + ((size_t)lc * nsc + slm[tt]) * ne2t<NN>();
+        const bool ok = grp * 4 + tt < A.nsc;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int r = h + 4 * m;
+          if (ok && r < NN && c < NN) zr[r * NN + c] = zm[tt][m];
+        }
+      }
       mprod<false>(ram, zm, pm, h, c);  // A ZT   (A symmetric: its own transpose)
       mprod<false>(tm, pm, ram, h, c);  // T (A ZT)
 #pragma unroll
@@ -715,6 +741,269 @@ __global__ __launch_bounds__(64, 1) void hd_team_mfma_sweep_kernel(SweepArgs A) 
   }
 }
 
+
+// ============================================================================
+// Intensity path, nstr 18..32: hd_rad.hip's per-unit adding sweep +
+// back-substitution (hd_rad_sweep_kernel: the stack state R_above/S_down and
+// I+/I- kept at every level) on the team layout with the dense products on the
+// matrix core -- four units (solve, azimuthal mode) per wave, the arithmetic of
+// hd_team_mfma_sweep_kernel above.  Reads and writes the radiance kernels'
+// unit-fastest records ([element][unit]: rsw, bsub, lev) unchanged, so the
+// per-lane kernels around it (hd_rad_wide.hip) need nothing new.  Replaces a
+// one-lane-per-unit loop whose 16 x 16 matrices lived in private memory
+// (62% of the nstr-32 radiance time, profiles/r03/).
+// ============================================================================
+template <int NN>
+__global__ __launch_bounds__(64, 1) void hd_rad_team_sweep_kernel(RadArgs A) {
+  __shared__ double lds[2 * kSet];
+  double* S0 = lds;
+  double* S1 = lds + kSet;
+  const Quad<NN>& Qc = tquad<NN>(c_qt);
+  constexpr int nsym = NN * (NN + 1) / 2;
+  constexpr int NE1 = rad_layer_record_doubles(NN);
+  constexpr int NB = rad_bsub_doubles(NN);
+  const int lane = (int)threadIdx.x;
+  const int h = lane >> 4, c = lane & 15;  // M layout
+  const int t = h, i = c;                  // T layout: team t, row i
+  const bool act = i < NN;
+  const int ii = act ? i : 0;
+  const int grp = (int)blockIdx.x;
+  // every lane takes part in the MFMA / LDS / DPP exchanges: a team past the end
+  // repeats the block's first unit and stores nothing
+  const bool valid = grp * 4 + t < A.nu;
+  const int u = valid ? grp * 4 + t : grp * 4;
+  const int m = u / A.ns;
+  const int sl = u - m * A.ns;
+  const long s = A.s0 + sl;
+  const int L = A.nlyr;
+  const size_t nu = A.nu;
+  int st = 0;
+  const double msk = act ? 1.0 : 0.0;
+  const double g_i = Qc.g[ii] * msk;
+  const double rg_i = Qc.rg[ii] * msk;
+  const bool wr = valid && act;
+
+  for (int k = lane; k < 2 * kSet; k += 64) lds[k] = 0.0;
+  lds_fence();
+
+  const double mu0 = A.umu0 ? umu0_floor(A.umu0[s]) : 1.0;
+  const double fb = A.fbeam ? A.fbeam[s] : 0.0;
+  const bool beam = fb > 0.0 && mu0 > 0.0;
+  double alb = A.albedo ? A.albedo[s] : 0.0;
+  if (!(alb >= 0.0) || !(alb <= 1.0)) st |= kStBadInput;
+  double top = A.fisot ? A.fisot[s] : 0.0;
+  double bsurf = 0.0;
+  if (A.planck) {
+    bsurf = A.planckv[(size_t)(L + 1) * A.ns + sl];
+    top += A.planckv[(size_t)(L + 2) * A.ns + sl];
+  }
+  if (m > 0) alb = top = bsurf = 0.0;  // Lambert surface, isotropic top: mode 0 only
+  const double rmu0 = beam ? 1.0 / mu0 : 0.0;
+  const double f0mu0 = (beam && m == 0) ? fb * mu0 : 0.0;
+
+  int um[4];  // the wave's four units (M layout)
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt) um[tt] = grp * 4 + tt < A.nu ? grp * 4 + tt : grp * 4;
+
+  double ram[4][4];  // R_above (M layout)
+  double ra[NN];     // R_above row i (T layout)
+  double sd = g_i * top;
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ram[tt][q] = 0.0;
+  sfor<0, NN>([&](auto J) { ra[HD_K(J)] = 0.0; });
+  double tauc = 0.0;
+
+  for (int lc = 0; lc < L; ++lc) {
+    const double* lp = A.rsw + (size_t)lc * NE1 * nu;  // element e of unit v: lp[e*nu + v]
+    double* bp = A.bsub + (size_t)lc * NB * nu;
+    // the stack above this layer: R_above (packed upper, row i from j = i) and S_down
+    if (wr) {
+      sfor<0, NN>([&](auto J) {
+        constexpr int j = HD_K(J);
+        if (j >= i) bp[(size_t)(NN * NN + NN + sym_index<NN>(i, j)) * nu + u] = ra[j];
+      });
+      bp[(size_t)(NN * NN + NN + nsym + i) * nu + u] = sd;
+    }
+    // R~, T~ (packed upper) of the four units in M layout; this unit's rows (T layout)
+    double rm[4][4], tm[4][4];
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = h + 4 * q;
+        const bool in = r < NN && c < NN;
+        const int e = in ? sym_index<NN>(r, c) : 0;
+        rm[tt][q] = in ? lp[(size_t)e * nu + um[tt]] : 0.0;
+        tm[tt][q] = in ? lp[(size_t)(nsym + e) * nu + um[tt]] : 0.0;
+      }
+    double rl[NN], tr[NN];
+    sfor<0, NN>([&](auto J) {
+      const int e = sym_index<NN>(ii, HD_K(J));
+      rl[HD_K(J)] = lp[(size_t)e * nu + u] * msk;
+      tr[HD_K(J)] = lp[(size_t)(nsym + e) * nu + u] * msk;
+    });
+    const double spl = lp[(size_t)(2 * nsym + ii) * nu + u] * msk;
+    const double sml = lp[(size_t)(2 * nsym + NN + ii) * nu + u] * msk;
+    // W1 = I - R A on the matrix core, to team rows through LDS
+    {
+      double pw[4][4];
+      mprod<false>(rm, ram, pw, h, c);
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pw[tt][q] = (h + 4 * q == c ? 1.0 : 0.0) - pw[tt][q];
+      lds_fence();
+      put_m(S0, h, c, pw);
+      lds_fence();
+    }
+    double w[NN];
+    get_rows<NN>(S0, t, i, w);
+    sfor<0, NN>([&](auto J) { w[HD_K(J)] *= msk; });
+    // t1 = R Sd + S+
+    double t1 = spl;
+    sfor<0, NN>([&](auto K) { t1 = fma(rl[HD_K(K)], bc<HD_K(K)>(sd), t1); });
+    // LU without pivoting; reciprocal pivots on the diagonal
+    sfor<0, NN>([&](auto K) {
+      constexpr int k = HD_K(K);
+      const double piv = bc<k>(w[k]);
+      if (!(fabs(piv) > 1.0e-12)) st |= kStPivot;
+      const double rp = rcp_nr(piv);
+      const double lik = w[k] * rp;
+      const double mm = i > k ? lik : 0.0;
+      w[k] = i == k ? rp : (i > k ? lik : w[k]);
+      sfor<k + 1, NN>([&](auto J) {
+        constexpr int j = HD_K(J);
+        w[j] = fma(-mm, bc<k>(w[j]), w[j]);
+      });
+    });
+    // t1 <- W1^-1 t1
+    sfor<0, NN>([&](auto K) {
+      constexpr int k = HD_K(K);
+      const double tk = bc<k>(t1);
+      if (i > k) t1 = fma(-w[k], tk, t1);
+    });
+    sfor_rev<0, NN>([&](auto K) {
+      constexpr int k = HD_K(K);
+      if (i == k) t1 *= w[k];
+      const double tk = bc<k>(t1);
+      if (i < k) t1 = fma(-w[k], tk, t1);
+    });
+    // u = A t1 + Sd
+    double uv = sd;
+    sfor<0, NN>([&](auto K) { uv = fma(ra[HD_K(K)], bc<HD_K(K)>(t1), uv); });
+    if (wr) bp[(size_t)(NN * NN + i) * nu + u] = t1;
+    // ZT = W1^-1 T = U^-1 (L^-1 T): columns of the triangular inverses on the team
+    // (lane i: row i of the transposed inverse), the products on the matrix core
+    {
+      double zl[NN], zu[NN];
+      sfor<0, NN>([&](auto R) {
+        constexpr int r = HD_K(R);
+        double v = i == r ? 1.0 : 0.0;
+        sfor<0, r>([&](auto K) { v = fma(-bc<r>(w[HD_K(K)]), zl[HD_K(K)], v); });
+        zl[r] = v;
+        pin<NN>(w);
+      });
+      sfor_rev<0, NN>([&](auto R) {
+        constexpr int r = HD_K(R);
+        double v = i == r ? 1.0 : 0.0;
+        sfor<r + 1, NN>([&](auto K) { v = fma(-bc<r>(w[HD_K(K)]), zu[HD_K(K)], v); });
+        zu[r] = v * bc<r>(w[r]);
+        pin<NN>(w);
+      });
+      sfor<0, NN>([&](auto J) {
+        zl[HD_K(J)] *= msk;
+        zu[HD_K(J)] *= msk;
+      });
+      lds_fence();
+      put_rows<NN>(S0, t, i, zl);  // L^-T
+      put_rows<NN>(S1, t, i, zu);  // U^-T
+    }
+    // Sd <- T u + S-
+    {
+      double tq = sml;
+      sfor<0, NN>([&](auto K) { tq = fma(tr[HD_K(K)], bc<HD_K(K)>(uv), tq); });
+      sd = tq * msk;
+    }
+    lds_fence();
+    {
+      double li[4][4], x1[4][4], zm[4][4], pm[4][4];
+      get_m(S0, h, c, li);
+      mprod<false>(li, tm, x1, h, c);  // L^-1 T
+      get_m(S1, h, c, li);
+      mprod<false>(li, x1, zm, h, c);  // ZT
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const bool ok = grp * 4 + tt < A.nu;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = h + 4 * q;
+          if (ok && r < NN && c < NN) bp[(size_t)(r * NN + c) * nu + um[tt]] = zm[tt][q];
+        }
+      }
+      mprod<false>(ram, zm, pm, h, c);  // A ZT
+      mprod<false>(tm, pm, ram, h, c);  // T (A ZT)
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ram[tt][q] += rm[tt][q];
+      lds_fence();
+      put_m(S0, h, c, ram);
+      lds_fence();
+    }
+    get_rows<NN>(S0, t, i, ra);
+    sfor<0, NN>([&](auto J) { ra[HD_K(J)] *= msk; });
+    tauc += lp[(size_t)(2 * nsym + 2 * NN) * nu + u];
+  }
+
+  // ---- Lambertian surface (mode 0): I+ = g x ----
+  double rgrow = 0.0;
+  sfor<0, NN>([&](auto J) { rgrow = fma(ra[HD_K(J)], Qc.g[HD_K(J)], rgrow); });
+  const double gsd = bc<0>(team_sum(g_i * sd));
+  const double grg = bc<0>(team_sum(g_i * rgrow));
+  double esurf = (1.0 - alb) * bsurf;
+  if (beam) esurf += alb * f0mu0 * exp(-tauc * rmu0) / kPi;
+  const double x = (2.0 * alb * gsd + esurf) / (1.0 - 2.0 * alb * grg);
+  double ip = g_i * x;
+  double chk = 0.0;
+  {
+    double dn = sd;
+    sfor<0, NN>([&](auto J) { dn = fma(ra[HD_K(J)], bc<HD_K(J)>(ip), dn); });
+    double* lv = A.lev + (size_t)L * 2 * NN * nu;
+    if (wr) {
+      lv[(size_t)i * nu + u] = x;
+      lv[(size_t)(NN + i) * nu + u] = dn * rg_i;
+    }
+    chk += dn * msk;
+  }
+  // ---- back-substitution bottom -> top, I+ and I- at every level ----
+  for (int lc = L - 1; lc >= 0; --lc) {
+    const double* bp = A.bsub + (size_t)lc * NB * nu;
+    double nip = bp[(size_t)(NN * NN + ii) * nu + u] * msk;
+    sfor<0, NN>([&](auto J) {
+      nip = fma(bp[(size_t)(ii * NN + HD_K(J)) * nu + u] * msk, bc<HD_K(J)>(ip), nip);
+    });
+    ip = nip;
+    double dn = bp[(size_t)(NN * NN + NN + nsym + ii) * nu + u] * msk;
+    sfor<0, NN>([&](auto J) {
+      const double r = bp[(size_t)(NN * NN + NN + sym_index<NN>(ii, HD_K(J))) * nu + u] * msk;
+      dn = fma(r, bc<HD_K(J)>(ip), dn);
+    });
+    double* lv = A.lev + (size_t)lc * 2 * NN * nu;
+    if (wr) {
+      lv[(size_t)i * nu + u] = ip * rg_i;
+      lv[(size_t)(NN + i) * nu + u] = dn * rg_i;
+    }
+    chk += ip + dn;
+  }
+  if (act && !isfinite(chk)) st |= kStNonFinite;
+  if (valid && st) {
+    atomicOr(&A.status[s], st);
+    if (st & 0x0F) atomicOr(A.anyerr, 1);
+  }
+}
+
 hipError_t upload_quad_tables_team_mfma(const QuadTablesTeam& t) {
   return hipMemcpyToSymbol(HIP_SYMBOL(c_qt), &t, sizeof(t), 0, hipMemcpyHostToDevice);
 }
@@ -757,6 +1046,28 @@ hipError_t launch_team_layer_mfma(int nn, const LayerArgs& la, hipStream_t strea
     case 14: return launch_layer<14>(la, stream);
     case 15: return launch_layer<15>(la, stream);
     case 16: return launch_layer<16>(la, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+
+template <int NN>
+static hipError_t launch_rad_sweep(const RadArgs& a, hipStream_t stream) {
+  hipLaunchKernelGGL(hd_rad_team_sweep_kernel<NN>, dim3((unsigned)((a.nu + 3) / 4)), dim3(64), 0,
+                     stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_rad_team_sweep(int nn, const RadArgs& a, hipStream_t stream) {
+  switch (nn) {
+    case 9: return launch_rad_sweep<9>(a, stream);
+    case 10: return launch_rad_sweep<10>(a, stream);
+    case 11: return launch_rad_sweep<11>(a, stream);
+    case 12: return launch_rad_sweep<12>(a, stream);
+    case 13: return launch_rad_sweep<13>(a, stream);
+    case 14: return launch_rad_sweep<14>(a, stream);
+    case 15: return launch_rad_sweep<15>(a, stream);
+    case 16: return launch_rad_sweep<16>(a, stream);
     default: return hipErrorInvalidValue;
   }
 }

@@ -3,7 +3,8 @@
 #   gpurun --timeout 1200 -- bash scripts/gpu.sh TAG STEP [STEP ...]
 # Steps run in order, each under its own time limit; the first failure ends the
 # call (nothing more touches the GPU after a failed step).  Outputs: gpurun_out/TAG/.
-#   tests[=SEL]          pytest -m gpu in one process (SEL: comma-separated selectors)
+#   tests[=SEL[@K]]      pytest -m gpu in one process (SEL: comma-separated selectors,
+#                        K: a -k expression with '+' for spaces)
 #   smoke                __graft_entry__.smoke()
 #   bench=NAME[:ARGS]    python bench.py ARGS              > bench_NAME.json
 #   stats=NAME[:ARGS]    rocprofv3 --kernel-trace --stats of bench.py ARGS:
@@ -12,6 +13,7 @@
 #                        scripts/pmc_run.py (one chunk of the C4 / C5 shape)
 #   sq=NAME[:NSTR]       SQ instruction-mix / MFMA / LDS passes over scripts/pmc_run.py
 #   rad=NAME[:ARGS]      python scripts/bench_rad.py ARGS  > rad_NAME.json
+#   radstats=NAME[:ARGS] rocprofv3 --kernel-trace --stats of scripts/bench_rad.py ARGS
 # ARGS are comma-separated (bench=c5:--config,c5,--steps,5).
 set -e -o pipefail
 TAG=${1:?tag}; shift
@@ -38,9 +40,12 @@ for step in "$@"; do
   [ "$rest" = "$val" ] && rest=""
   case $kind in
     tests)
-      sel=$(args_of "${val:-tests}")
-      say "pytest -m gpu $sel"
-      timeout -k 10 840 python -u -m pytest $sel -m gpu -x -v --timeout 120 \
+      v=${val:-tests}
+      sel=$(args_of "${v%%@*}")
+      kexpr=""
+      [ "${v#*@}" != "$v" ] && kexpr=${v#*@} && kexpr=${kexpr//+/ }
+      say "pytest -m gpu $sel ${kexpr:+-k \"$kexpr\"}"
+      timeout -k 10 840 python -u -m pytest $sel -m gpu ${kexpr:+-k "$kexpr"} -x -v --timeout 120 \
         --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || { tail -40 "$OUT/pytest_gpu.log"; exit 1; }
       tail -3 "$OUT/pytest_gpu.log" ;;
     smoke)
@@ -77,6 +82,12 @@ for step in "$@"; do
       timeout -k 10 420 python scripts/bench_rad.py $(args_of "$rest") > "$OUT/rad_$name.json" \
         2> "$OUT/rad_$name.err" || { tail -20 "$OUT/rad_$name.err"; exit 1; }
       cat "$OUT/rad_$name.json" ;;
+    radstats)
+      say "rocprofv3 --kernel-trace --stats bench_rad.py $(args_of "$rest")"
+      timeout -k 10 480 rocprofv3 --kernel-trace --stats -d "$OUT/radstats_$name" -o kt \
+        --output-format csv -- python3 scripts/bench_rad.py $(args_of "$rest") \
+        > "$OUT/radstats_$name.json" 2> "$OUT/radstats_$name.err" || { tail -20 "$OUT/radstats_$name.err"; exit 1; }
+      cat "$OUT/radstats_$name.json" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
