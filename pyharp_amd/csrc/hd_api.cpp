@@ -187,6 +187,7 @@ int ensure_rad_tables(hd_context* ctx) {
   std::lock_guard<std::mutex> lk(g_tab_mu);
   if (g_rad_tables[ctx->device]) return HD_OK;
   hipError_t e = hd::upload_rad_tables(quad_host());
+  if (e == hipSuccess) e = hd::upload_rad_tables_team(quad_host());
   if (e != hipSuccess)
     return fail(ctx, HD_EHIP, "hd_solve_radiance: constant upload: %s", hipGetErrorString(e));
   g_rad_tables[ctx->device] = true;

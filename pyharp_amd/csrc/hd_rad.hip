@@ -1562,7 +1562,10 @@ static void launch_rad(const RadArgs& a, bool radiances, hipStream_t st) {
   hipLaunchKernelGGL(hd_rad_taus_kernel, dim3(ns_b), dim3(256), 0, st, a);
   const unsigned nb1 = (unsigned)(((a.nu + 63) / 64) *
                                   ((a.nlyr + kLayersPerBlockR - 1) / kLayersPerBlockR));
-  hipLaunchKernelGGL(hd_rad_layer_kernel<NN>, dim3(nb1), dim3(kLayerBlockR), 0, st, a);
+  if constexpr (NN > kMaxRegNN)
+    (void)hd::launch_rad_team_layer(NN, a, st);  // team layout + MFMA (hd_team_mfma.hip)
+  else
+    hipLaunchKernelGGL(hd_rad_layer_kernel<NN>, dim3(nb1), dim3(kLayerBlockR), 0, st, a);
   if constexpr (NN > kMaxRegNN)
     (void)hd::launch_rad_team_sweep(NN, a, st);  // team layout + MFMA (hd_team_mfma.hip)
   else

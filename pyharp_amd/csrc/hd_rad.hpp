@@ -79,6 +79,10 @@ size_t rad_scratch_doubles_per_unit(int nn, int nlyr);
 // nstr 18..32: the adding sweep + back-substitution on the team layout with the
 // dense products on FP64 MFMA, four units per wave (hd_team_mfma.hip)
 hipError_t launch_rad_team_sweep(int nn, const RadArgs& a, hipStream_t stream);
+// nstr 18..32: the per-(unit, layer) setup on the team layout + FP64 MFMA, and its
+// Y_l^m tables (uploaded with the other intensity-path tables)
+hipError_t launch_rad_team_layer(int nn, const RadArgs& a, hipStream_t stream);
+hipError_t upload_rad_tables_team(const QuadHost* per_nn);
 // nstr 18..32: the same kernels compiled with rolled NN-loops (hd_rad_wide.hip)
 namespace wide {
 hipError_t upload_rad_tables(const QuadHost* per_nn);

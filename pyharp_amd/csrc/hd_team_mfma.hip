@@ -32,6 +32,8 @@
 // Replaces the DPP-broadcast products of hd_team_layer_kernel, whose row
 // broadcasts, 64-bit selects and register spills were 39% of its VALU
 // instructions at one wave per SIMD (profiles/r02_c5_team_counters_v1.json).
+#include <cmath>
+
 #include "hd_rad.hpp"
 #include "hd_team_prims.hpp"
 
@@ -131,6 +133,41 @@ __device__ __forceinline__ int block_logical() {
 }
 __device__ __forceinline__ int block_group(int L) { return block_logical() / L; }
 __device__ __forceinline__ int block_layer(int L) { return block_logical() % L; }
+
+
+// Y_l^m(mu_i) tables of nstr 18..32 for the intensity path's team kernels (mode
+// m, degree l < nstr, node i) and the Y_l^m recurrence coefficients; filled
+// from the same host recurrence as hd_rad.hip's tables (upload_rad_tables_team)
+template <int NN>
+struct RadTabTeam {
+  double lam[2 * NN][2 * NN][NN];
+};
+struct RadTabsTeam {
+  RadTabTeam<9> t9;
+  RadTabTeam<10> t10;
+  RadTabTeam<11> t11;
+  RadTabTeam<12> t12;
+  RadTabTeam<13> t13;
+  RadTabTeam<14> t14;
+  RadTabTeam<15> t15;
+  RadTabTeam<16> t16;
+  double seed[2 * kMaxNN];               // prod_{a<=m} sqrt((2a-1)/(2a))
+  double ra[2 * kMaxNN][2 * kMaxNN];     // (2l-1)/sqrt(l^2-m^2), l > m
+  double rb[2 * kMaxNN][2 * kMaxNN];     // sqrt((l-1)^2-m^2)/sqrt(l^2-m^2), l > m
+};
+__constant__ RadTabsTeam c_rtt;
+
+template <int NN>
+__device__ __forceinline__ const double* rad_lam(int m) {
+  if constexpr (NN == 9) return &c_rtt.t9.lam[m][0][0];
+  else if constexpr (NN == 10) return &c_rtt.t10.lam[m][0][0];
+  else if constexpr (NN == 11) return &c_rtt.t11.lam[m][0][0];
+  else if constexpr (NN == 12) return &c_rtt.t12.lam[m][0][0];
+  else if constexpr (NN == 13) return &c_rtt.t13.lam[m][0][0];
+  else if constexpr (NN == 14) return &c_rtt.t14.lam[m][0][0];
+  else if constexpr (NN == 15) return &c_rtt.t15.lam[m][0][0];
+  else return &c_rtt.t16.lam[m][0][0];
+}
 
 // lane i of each team: column i of the inverse of the lower-triangular J whose
 // rows the team holds (forward substitution J z = e_i), i.e. row i of J^-T
@@ -742,6 +779,385 @@ __global__ __launch_bounds__(64, 1) void hd_team_mfma_sweep_kernel(SweepArgs A) 
 }
 
 
+
+// ============================================================================
+// Intensity path, nstr 18..32: hd_rad.hip's per-(unit, layer) setup
+// (hd_rad_layer_kernel: the flux layer setup for azimuthal mode m with the
+// Y_l^m(mu_i) tables, parity of l+m, beam source x (2 - delta_m0), thermal only
+// at m = 0, plus L, V, k, the particular solution and the exponentials kept for
+// the radiance kernels) on the team layout with the dense products on the matrix
+// core: hd_team_mfma_layer_kernel's algebra, four units per wave.  Writes the
+// radiance kernels' unit-fastest records (rsw: R~/T~ packed upper, S~+-, tau';
+// rrd: L packed, V, k, Z+-, h, B_top, dB/dtau', tau', omega', e^{-k tau'},
+// e^{-tau'/mu0}) exactly as hd_rad_layer_kernel lays them out.
+// ============================================================================
+template <int NN>
+__global__ __launch_bounds__(64, 1) void hd_rad_team_layer_kernel(RadArgs A) {
+  __shared__ double lds[2 * kSet + 4 * 2 * 16];
+  double* S0 = lds;
+  double* S1 = lds + kSet;
+  double* G = lds + 2 * kSet;  // [t][dsq | gsq][16]
+  constexpr int N = 2 * NN;
+  constexpr int nsym = NN * (NN + 1) / 2;
+  constexpr int NE1 = rad_layer_record_doubles(NN);
+  constexpr int NR = rad_rec_doubles(NN);
+  constexpr int oV = nsym, oK = nsym + NN * NN, oZp = oK + NN, oZm = oZp + NN, oH = oZm + NN;
+  constexpr int oBt = oH + NN, oSl = oBt + 1, oTp = oSl + 1, oOm = oTp + 1, oEk = oOm + 1;
+  constexpr int oE0 = oEk + NN;
+  const Quad<NN>& Qc = tquad<NN>(c_qt);
+  const int lane = (int)threadIdx.x;
+  const int h = lane >> 4, c = lane & 15;  // M layout
+  const int t = h, i = c;                  // T layout: team t, row i
+  const bool act = i < NN;
+  const int ii = act ? i : 0;
+  const int L = A.nlyr;
+  const size_t nu = A.nu;
+  // block = 4 consecutive units of one layer, blocks numbered layer-fastest and
+  // XCD-aware as in the flux kernel
+  const int grp = block_group(L);
+  const int lc = block_layer(L);
+  const bool valid = grp * 4 + t < A.nu;
+  const int u = valid ? grp * 4 + t : grp * 4;
+  const int m = u / A.ns;
+  const int sl = u - m * A.ns;
+  const long s = A.s0 + sl;
+  const int nm = A.nmom;
+  const int np = A.nprop;
+  const bool wr = valid && act;
+  int st = 0;
+  int um[4];
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt) um[tt] = grp * 4 + tt < A.nu ? grp * 4 + tt : grp * 4;
+  double* rr = A.rrd + (size_t)lc * NR * nu + u;   // element e: rr[e * nu]
+  double* out = A.rsw + (size_t)lc * NE1 * nu;    // element e of unit v: out[e * nu + v]
+
+  for (int k = lane; k < 2 * kSet; k += 64) lds[k] = 0.0;
+  lds_fence();
+
+  const double msk = act ? 1.0 : 0.0;
+  const double mu_i = fma(msk, Qc.mu[ii] - 1.0, 1.0);
+  const double sd_i = Qc.sd[ii] * msk;
+  const double g_i = Qc.g[ii] * msk;
+  const double rmu_i = Qc.rmu[ii] * msk;
+  const double rg_i = Qc.rg[ii] * msk;
+
+  // ---- inputs of this layer (harp layer L-1-lc) + delta-M (c_setdis) ----
+  const double* q = A.prop + ((size_t)s * L + (L - 1 - lc)) * np;
+  const double tau = q[0];
+  double ssa = np > 1 ? q[1] : 0.0;
+  if (!(tau >= 0.0) || !(ssa >= 0.0) || !(ssa <= 1.0)) st |= kStBadInput;
+  if (ssa == 1.0) ssa = 1.0 - kDither;
+  const double f = nm >= N ? q[1 + N] : 0.0;
+  if (!(f < 1.0)) st |= kStBadInput;
+  const double taup = (1.0 - ssa * f) * tau;
+  const double om = ssa * (1.0 - f) / (1.0 - ssa * f);
+  const double rf = om / (1.0 - f);
+
+  const double mu0 = A.umu0 ? umu0_floor(A.umu0[s]) : 1.0;
+  const double fb = A.fbeam ? A.fbeam[s] : 0.0;
+  const bool beam = fb > 0.0 && mu0 > 0.0;
+  if (fb > 0.0 && !(mu0 <= 1.0)) st |= kStBadInput;
+  const double rmu0 = beam ? 1.0 / mu0 : 0.0;
+  const double mub = beam ? mu0 : 0.0;
+  const bool therm = A.planck && m == 0;
+
+  // ---- mode-m phase-matrix rows (parity of l+m): S+ (ap), S- (lch); beam sums ----
+  double ap[NN], lch[NN];
+  double xs = 0.0, xd = 0.0;
+  sfor<0, NN>([&](auto J) { ap[HD_K(J)] = lch[HD_K(J)] = 0.0; });
+  {
+    const int mp = m & 1;
+    const double* lam = rad_lam<NN>(m);
+    const double sx = sqrt(fmax(0.0, 1.0 - mub * mub));
+    double seed = c_rtt.seed[m];
+    for (int a = 0; a < m; ++a) seed *= sx;  // Y_m^m(mu0)
+    double y1 = 0.0, y2 = 0.0;                // Y_{l-1}^m(mu0), Y_{l-2}^m(mu0)
+#pragma nounroll
+    for (int l2 = 0; l2 < NN; ++l2) {
+      const int la = 2 * l2, lb = la + 1;
+      const double ya =
+          la < m ? 0.0 : (la == m ? seed : fma(c_rtt.ra[m][la] * mub, y1, -c_rtt.rb[m][la] * y2));
+      y2 = y1;
+      y1 = ya;
+      const double yb =
+          lb < m ? 0.0 : (lb == m ? seed : fma(c_rtt.ra[m][lb] * mub, y1, -c_rtt.rb[m][lb] * y2));
+      y2 = y1;
+      y1 = yb;
+      const int le = mp ? lb : la, lo = mp ? la : lb;
+      const double pe0 = mp ? yb : ya, po0 = mp ? ya : yb;
+      const double che = le == 0 ? 1.0 : (le <= nm ? q[1 + le] : 0.0);
+      const double cho = lo == 0 ? 1.0 : (lo <= nm ? q[1 + lo] : 0.0);
+      const double ge = (2 * le + 1) * (che - f) * rf;
+      const double go = (2 * lo + 1) * (cho - f) * rf;
+      const double te = lam[le * NN + ii] * msk;  // Y_le^m(mu_i), this lane's node
+      const double to = lam[lo * NN + ii] * msk;
+      const double ue = ge * te;
+      const double uo = go * to;
+      xs = fma(ue, pe0, xs);
+      xd = fma(uo, po0, xd);
+      sfor<0, NN>([&](auto J) {
+        constexpr int j = HD_K(J);
+        ap[j] = fma(ue, bc<j>(te), ap[j]);
+        lch[j] = fma(uo, bc<j>(to), lch[j]);
+      });
+    }
+  }
+  sfor<0, NN>([&](auto J) {
+    constexpr int j = HD_K(J);
+    const double diag = i == j ? rmu_i : 0.0;
+    const double sij = sd_i * Qc.sd[j];
+    lch[j] = fma(-sij, lch[j], diag);
+    ap[j] = fma(-sij, ap[j], diag);
+  });
+  // L L^T = S-
+  double lt[NN], rdl;
+  if (!team_chol<NN, true>(lch, lt, rdl)) st |= kStEigen;
+  if (wr) {  // L, packed lower row-major: row i holds lch[k], k <= i
+    sfor<0, NN>([&](auto K) {
+      constexpr int k = HD_K(K);
+      if (k <= i) rr[(size_t)(i * (i + 1) / 2 + k) * nu] = lch[k];
+    });
+  }
+
+  // ---- pre-Jacobi vectors (depend on L only) ----
+  double w2 = 0.0, lxd = 0.0;
+  const double fb2 = fb * ((m == 0 ? 0.5 : 1.0) / kPi);
+  if (beam) {
+    const double y = sd_i * (fb2 * xs);
+    double z = 0.0;  // z = L^T y
+    sfor<0, NN>([&](auto K) { z = fma(lt[HD_K(K)], bc<HD_K(K)>(y), z); });
+    const double yl = team_matvec<NN>(lch, z);  // L z
+    const double xdi = -fb2 * xd;
+    const double rv = fma(-yl, rg_i, xdi * rmu0 * rmu_i);
+    w2 = g_i * rv;
+    lxd = sd_i * xdi;
+    team_lsolve<NN>(lch, rdl, w2);
+    team_usolve<NN>(lt, rdl, w2);
+    team_lsolve<NN>(lch, rdl, lxd);
+    team_usolve<NN>(lt, rdl, lxd);
+  }
+  double cvec = 0.0, db = 0.0, bsum = 0.0;
+  if (therm) {
+    const double bt = A.planckv[(size_t)(L - lc) * A.ns + sl];
+    const double bb = taup > 0.0 ? A.planckv[(size_t)(L - lc - 1) * A.ns + sl] : bt;
+    db = bb - bt;
+    bsum = bt + bb;
+    const double b1 = taup > 0.0 ? 2.0 * db / taup : 0.0;
+    cvec = sd_i * mu_i;
+    team_lsolve<NN>(lch, rdl, cvec);
+    team_usolve<NN>(lt, rdl, cvec);
+    if (wr) rr[(size_t)(oH + i) * nu] = rg_i * cvec;
+    cvec = fma(b1 * rg_i, cvec, db) * msk;
+    if (valid && i == 0) {
+      rr[(size_t)oBt * nu] = bt;
+      rr[(size_t)oSl * nu] = 0.5 * b1;
+    }
+  } else {
+    if (wr) rr[(size_t)(oH + i) * nu] = 0.0;
+    if (valid && i == 0) {
+      rr[(size_t)oBt * nu] = 0.0;
+      rr[(size_t)oSl * nu] = 0.0;
+    }
+  }
+  if (valid && i == 0) {
+    rr[(size_t)oTp * nu] = taup;
+    rr[(size_t)oOm * nu] = om;
+  }
+  {
+    double z[NN];
+    team_tri_inverse_col<NN>(lch, rdl, z);  // row i of L^-T -> S0 (lch dies here)
+    put_rows<NN>(S0, t, i, z);
+  }
+
+  // ---- C C^T = S+ ; B0 = C^T L (lane j: column j) ; C^-1 to LDS ----
+  double bcol[NN];
+  {
+    double unused[NN], rdc;
+    if (!team_chol<NN, false>(ap, unused, rdc)) st |= kStEigen;
+    sfor<0, NN>([&](auto I) {
+      constexpr int r = HD_K(I);
+      double uu = 0.0;
+      sfor<r, NN>([&](auto K) { uu = fma(bc<HD_K(K)>(ap[r]), lt[HD_K(K)], uu); });
+      bcol[r] = uu;
+      pin<NN>(ap);
+    });
+    double z[NN];
+    team_tri_inverse_col<NN>(ap, rdc, z);  // row i of C^-T -> S1
+    put_rows<NN>(S1, t, i, z);
+  }
+
+  // ---- eigenpairs: Sym = L^T S+ L = B0^T B0 = V diag(k^2) V^T ----
+  lds_fence();
+  if (!team_jacobi<NN>(bcol, A.max_sweeps)) st |= kStEigen;
+  lds_fence();
+  double kk;
+  {
+    double k2 = 0.0;
+    sfor<0, NN>([&](auto K) { k2 = fma(bcol[HD_K(K)], bcol[HD_K(K)], k2); });
+    if (act && !(k2 > 0.0)) st |= kStEigen;
+    kk = sqrt(k2 > 0.0 ? k2 : 0.0) * msk;
+    const double x = kk * taup;
+    const double mm = -expm1(-x);
+    const double th = mm * rcp_nr(2.0 - mm);
+    const double delta = x > 1.0e-8 ? th * rcp_nr(kk > 0.0 ? kk : 1.0) : 0.5 * taup;
+    G[t * 32 + i] = sqrt(delta) * msk;
+    G[t * 32 + 16 + i] = sqrt(kk * th) * msk;
+    if (wr) {
+      rr[(size_t)(oK + i) * nu] = kk;
+      rr[(size_t)(oEk + i) * nu] = 1.0 - mm;  // exp(-k tau')
+    }
+  }
+
+  // ---- the dense products on the matrix core; V = L^-1 U; the beam solution ----
+  double zp = 0.0, zm = 0.0, e0 = 0.0;
+  {
+    double X[4][4], Y[4][4], U[4][4], UT[4][4];
+    {
+      double LiT[4][4];
+      get_m(S0, h, c, LiT);         // L^-T (M): the A^T operand of L^-1 (.)
+      get_mt(S0, h, c, X);          // L^-1 (M)
+      mprod<false>(X, X, Y, h, c);  // W = L^-T L^-1
+      get_mt(S1, h, c, X);          // C^-1 (M)
+      lds_fence();
+      put_m(S0, h, c, Y);            // W, row-major
+      put_rows<NN>(S1, t, i, bcol);  // rows of B^T
+      lds_fence();
+      get_mt(S1, h, c, Y);           // B (M)
+      mprod<false>(X, Y, U, h, c);   // U = C^-T B
+      mprod<false>(Y, X, UT, h, c);  // U^T = B^T C^-1
+      mprod<false>(LiT, U, X, h, c); // V = L^-1 U (M) -> the record, row-major
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const bool ok = grp * 4 + tt < A.nu;
+        double* rv = A.rrd + (size_t)lc * NR * nu + um[tt];
+#pragma unroll
+        for (int q2 = 0; q2 < 4; ++q2) {
+          const int r = h + 4 * q2;
+          if (ok && r < NN && c < NN) rv[(size_t)(oV + r * NN + c) * nu] = X[tt][q2];
+        }
+      }
+    }
+    lds_fence();
+    put_m(S1, h, c, UT);
+    lds_fence();
+    if (beam) {
+      double r_[NN];
+      get_rows<NN>(S1, t, i, r_);
+      const double r2 = rmu0 * rmu0;
+      const double tv = team_matvec<NN>(r_, w2);
+      double den = fma(-kk, kk, r2);
+      if (act && fabs(den) < 1.0e-9 * r2) {
+        st |= kStResonance;
+        den = den < 0.0 ? -1.0e-9 * r2 : 1.0e-9 * r2;
+      }
+      const double ttv = tv / den * msk;
+      get_cols<NN>(S1, t, i, r_);
+      const double sv = team_matvec<NN>(r_, ttv) * rg_i;
+      get_rows<NN>(S0, t, i, r_);
+      const double yy = team_matvec<NN>(r_, sd_i * mu_i * sv);
+      const double tauc = A.tauc[(size_t)lc * A.ns + sl];
+      const double att = 0.5 * exp(-tauc * rmu0);
+      const double dd = rg_i * fma(-yy, rmu0, lxd);
+      zp = (sv + dd) * att;
+      zm = (sv - dd) * att;
+      e0 = exp(-taup * rmu0);
+    }
+    if (wr) {
+      rr[(size_t)(oZp + i) * nu] = zp;
+      rr[(size_t)(oZm + i) * nu] = zm;
+    }
+    if (valid && i == 0) rr[(size_t)oE0 * nu] = e0;
+    get_m(S0, h, c, Y);            // W (M)
+    mprod<false>(U, Y, X, h, c);   // U^T W
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+      for (int q2 = 0; q2 < 4; ++q2) {
+        X[tt][q2] *= G[tt * 32 + 16 + h + 4 * q2];
+        UT[tt][q2] *= G[tt * 32 + h + 4 * q2];
+      }
+    mprod<true>(UT, UT, U, h, c);  // I + Omega Omega^T
+    mprod<true>(X, X, Y, h, c);    // I + Psi^T Psi
+    lds_fence();
+    put_m(S0, h, c, U);
+    put_m(S1, h, c, Y);
+    lds_fence();
+  }
+  const double ga = g_i * (cvec - fma(-zp, e0, zm));
+  const double gb = g_i * (fma(zp, e0, zm) + bsum);
+
+  // ---- A- = (I + Omega Omega^T)^-1, A+ = (I + Psi^T Psi)^-1 ----
+  double Am[4][4], Ap[4][4];
+  double pv, qv;
+  {
+    double hr[NN], unused[NN], z[NN], jrd, X[4][4];
+    get_rows<NN>(S0, t, i, hr);
+    if (!team_chol<NN, false>(hr, unused, jrd)) st |= kStEigen;
+    team_tri_inverse_col<NN>(hr, jrd, z);
+    lds_fence();
+    put_rows<NN>(S0, t, i, z);
+    lds_fence();
+    get_mt(S0, h, c, X);
+    mprod<false>(X, X, Am, h, c);
+    lds_fence();
+    put_m(S0, h, c, Am);
+    lds_fence();
+    get_rows<NN>(S0, t, i, hr);
+    pv = ga - team_matvec<NN>(hr, ga);
+    get_rows<NN>(S1, t, i, hr);
+    if (!team_chol<NN, false>(hr, unused, jrd)) st |= kStEigen;
+    team_tri_inverse_col<NN>(hr, jrd, z);
+    lds_fence();
+    put_rows<NN>(S1, t, i, z);
+    lds_fence();
+    get_mt(S1, h, c, X);
+    mprod<false>(X, X, Ap, h, c);
+    lds_fence();
+    put_m(S1, h, c, Ap);
+    lds_fence();
+    get_rows<NN>(S1, t, i, hr);
+    qv = team_matvec<NN>(hr, gb) - gb;
+  }
+
+  // ---- store: R~ = A+ - A-, T~ = A- + A+ - I packed upper (M layout), S~+-, tau' ----
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt) {
+    double chk = 0.0;
+    const bool ok = grp * 4 + tt < A.nu;
+#pragma unroll
+    for (int q2 = 0; q2 < 4; ++q2) {
+      const int r = h + 4 * q2;
+      const double rrv = Ap[tt][q2] - Am[tt][q2];
+      const double trv = (Am[tt][q2] + Ap[tt][q2]) - (r == c ? 1.0 : 0.0);
+      if (ok && r <= c && c < NN) {
+        const int e = sym_index<NN>(r, c);
+        out[(size_t)e * nu + um[tt]] = rrv;
+        out[(size_t)(nsym + e) * nu + um[tt]] = trv;
+      }
+      chk += rrv + trv;
+    }
+    if (ok && !isfinite(chk)) {
+      const int vt = um[tt];
+      atomicOr(&A.status[A.s0 + (vt - (vt / A.ns) * A.ns)], kStNonFinite);
+      atomicOr(A.anyerr, 1);
+    }
+  }
+  double chk = 0.0;
+  const double sp = g_i * (zp * (1.0 - e0) - db) + pv - qv;
+  const double sm = g_i * (-zm * (1.0 - e0) + db) - pv - qv;
+  if (wr) {
+    out[(size_t)(2 * nsym + i) * nu + u] = sp;
+    out[(size_t)(2 * nsym + NN + i) * nu + u] = sm;
+  }
+  chk += sp + sm;
+  if (valid && i == 0) out[(size_t)(2 * nsym + 2 * NN) * nu + u] = taup;
+  if (act && !isfinite(chk + taup)) st |= kStNonFinite;
+  if (valid && st) {
+    atomicOr(&A.status[s], st);
+    if (st & 0x0F) atomicOr(A.anyerr, 1);
+  }
+}
+
 // ============================================================================
 // Intensity path, nstr 18..32: hd_rad.hip's per-unit adding sweep +
 // back-substitution (hd_rad_sweep_kernel: the stack state R_above/S_down and
@@ -1070,6 +1486,79 @@ hipError_t launch_rad_team_sweep(int nn, const RadArgs& a, hipStream_t stream) {
     case 16: return launch_rad_sweep<16>(a, stream);
     default: return hipErrorInvalidValue;
   }
+}
+
+
+template <int NN>
+static hipError_t launch_rad_layer(const RadArgs& a, hipStream_t stream) {
+  const unsigned nb = (unsigned)(((a.nu + 3) / 4) * (long)a.nlyr);
+  hipLaunchKernelGGL(hd_rad_team_layer_kernel<NN>, dim3(nb), dim3(64), 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_rad_team_layer(int nn, const RadArgs& a, hipStream_t stream) {
+  switch (nn) {
+    case 9: return launch_rad_layer<9>(a, stream);
+    case 10: return launch_rad_layer<10>(a, stream);
+    case 11: return launch_rad_layer<11>(a, stream);
+    case 12: return launch_rad_layer<12>(a, stream);
+    case 13: return launch_rad_layer<13>(a, stream);
+    case 14: return launch_rad_layer<14>(a, stream);
+    case 15: return launch_rad_layer<15>(a, stream);
+    case 16: return launch_rad_layer<16>(a, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int NN>
+static void fill_rad_team(RadTabTeam<NN>& t, const QuadHost& h) {
+  for (int m = 0; m < 2 * NN; ++m)
+    for (int i = 0; i < NN; ++i) {
+      const double x = h.mu[i];
+      double seed = 1.0;
+      for (int a = 1; a <= m; ++a) seed *= std::sqrt((2.0 * a - 1) / (2.0 * a));
+      seed *= std::pow(std::sqrt(std::fmax(0.0, 1.0 - x * x)), m);
+      double y1 = 0.0, y2 = 0.0;
+      for (int l = 0; l < 2 * NN; ++l) {
+        double v = 0.0;
+        if (l == m) v = seed;
+        else if (l > m)
+          v = ((2.0 * l - 1) * x * y1 - std::sqrt((double)(l - 1) * (l - 1) - (double)m * m) * y2) /
+              std::sqrt((double)l * l - (double)m * m);
+        t.lam[m][l][i] = v;
+        y2 = y1;
+        y1 = v;
+      }
+    }
+}
+
+// the Y_l^m tables of the team intensity kernels (hd_rad.hip's recurrence); called
+// once per device under hd_api.cpp's global table lock
+hipError_t upload_rad_tables_team(const QuadHost* per_nn) {
+  static RadTabsTeam c;  // ~570 KB: keep off the stack
+  fill_rad_team<9>(c.t9, per_nn[8]);
+  fill_rad_team<10>(c.t10, per_nn[9]);
+  fill_rad_team<11>(c.t11, per_nn[10]);
+  fill_rad_team<12>(c.t12, per_nn[11]);
+  fill_rad_team<13>(c.t13, per_nn[12]);
+  fill_rad_team<14>(c.t14, per_nn[13]);
+  fill_rad_team<15>(c.t15, per_nn[14]);
+  fill_rad_team<16>(c.t16, per_nn[15]);
+  for (int m = 0; m < 2 * kMaxNN; ++m) {
+    double sd = 1.0;
+    for (int a = 1; a <= m; ++a) sd *= std::sqrt((2.0 * a - 1) / (2.0 * a));
+    c.seed[m] = sd;
+    for (int l = 0; l < 2 * kMaxNN; ++l) {
+      if (l > m) {
+        const double den = std::sqrt((double)l * l - (double)m * m);
+        c.ra[m][l] = (2.0 * l - 1) / den;
+        c.rb[m][l] = std::sqrt((double)(l - 1) * (l - 1) - (double)m * m) / den;
+      } else {
+        c.ra[m][l] = c.rb[m][l] = 0.0;
+      }
+    }
+  }
+  return hipMemcpyToSymbol(HIP_SYMBOL(c_rtt), &c, sizeof(RadTabsTeam), 0, hipMemcpyHostToDevice);
 }
 
 }  // namespace hd
