@@ -36,6 +36,10 @@ namespace harp_amd {
 
 class NetCDF4 {
  public:
+  // structural bounds of a file this reader trusts (user-supplied files: a cycle
+  // of continuation blocks or B-tree children must end in an error, not a hang)
+  static constexpr size_t kMaxBlocks = 4096;  // object-header continuation blocks
+  static constexpr int kMaxDepth = 64;       // B-tree levels
   struct Dataset {
     std::vector<uint64_t> dims;
     int tclass = -1;  // 0 fixed point, 1 float
@@ -174,6 +178,7 @@ class NetCDF4 {
       p += w;
       std::vector<std::pair<uint64_t, uint64_t>> blocks{{p, p + sz}};
       for (size_t b = 0; b < blocks.size(); ++b) {
+        if (b >= kMaxBlocks) bad("object header: too many continuation blocks (cycle?)");
         uint64_t q = blocks[b].first;
         const uint64_t end = blocks[b].second;
         const int hdr = (flags & 0x04) ? 6 : 4;
@@ -185,6 +190,7 @@ class NetCDF4 {
           if (type == 0x10) {
             const uint64_t off = abs_(le(d, so_)), len = le(d + so_, sl_);
             if (!sig(off, "OCHK")) bad("object header continuation");
+            if (len < 8) bad("object header continuation length");
             blocks.push_back({off + 4, off + len - 4});
           } else {
             out.push_back({type, d, size});
@@ -197,6 +203,7 @@ class NetCDF4 {
       std::vector<std::pair<uint64_t, uint64_t>> blocks{{a + 16, a + 16 + size}};
       uint64_t seen = 0;
       for (size_t b = 0; b < blocks.size() && seen < nmsg; ++b) {
+        if (b >= kMaxBlocks) bad("object header: too many continuation blocks (cycle?)");
         uint64_t q = blocks[b].first;
         while (q + 8 <= blocks[b].second && seen < nmsg) {
           const int type = (int)le(q, 2);
@@ -241,7 +248,8 @@ class NetCDF4 {
     if (!any) bad("root object is not a group");
   }
 
-  void walk_group_btree(uint64_t node, uint64_t names) {
+  void walk_group_btree(uint64_t node, uint64_t names, int depth = 0) {
+    if (depth > kMaxDepth) bad("group B-tree deeper than " + std::to_string(kMaxDepth));
     if (!sig(node, "TREE")) bad("group B-tree node");
     const int level = buf_[node + 5];
     const uint64_t n = le(node + 6, 2);
@@ -249,7 +257,7 @@ class NetCDF4 {
     for (uint64_t i = 0; i < n; ++i, p += so_ + sl_) {
       const uint64_t child = abs_(le(p, so_));
       if (level > 0) {
-        walk_group_btree(child, names);
+        walk_group_btree(child, names, depth + 1);
         continue;
       }
       if (!sig(child, "SNOD")) bad("symbol table node");
@@ -368,6 +376,8 @@ class NetCDF4 {
     const int depth = (int)le(bthd + 12, 2);
     const uint64_t root = abs_(le(bthd + 16, so_));
     const uint64_t root_n = le(bthd + 16 + so_, 2);
+    if (rec <= 0 || node_size <= 10 + (uint64_t)rec) bad("v2 B-tree record / node size");
+    if (depth > kMaxDepth) bad("v2 B-tree deeper than " + std::to_string(kMaxDepth));
     // per-depth record counts and their encoded sizes (H5B2__hdr_init)
     std::vector<uint64_t> max_nrec(depth + 1), cum(depth + 1);
     std::vector<int> cum_size(depth + 1, 0);
@@ -542,6 +552,7 @@ class NetCDF4 {
         data.swap(out);
       } else if (id == 2) {  // shuffle
         const size_t es = d.filters[f].second.empty() ? d.tsize : d.filters[f].second[0];
+        if (es == 0) bad("shuffle: element size 0");
         const size_t ne = data.size() / es;
         std::vector<uint8_t> out(data.size());
         for (size_t b = 0; b < es; ++b)
@@ -611,6 +622,9 @@ class NetCDF4 {
       }
     };
     if (rank == 0) bad("chunked scalar");
+    if ((int)d.chunk.size() != rank) bad("chunk rank differs from the dataspace rank");
+    for (uint64_t cdim : d.chunk)
+      if (cdim == 0) bad("chunk dimension 0");
     std::vector<uint64_t> grid(rank);
     uint64_t nchunks = 1;
     for (int k = 0; k < rank; ++k) {
@@ -657,7 +671,8 @@ class NetCDF4 {
   }
 
   template <class Place>
-  void btree_chunks(Dataset const& d, uint64_t node, int rank, Place& place) const {
+  void btree_chunks(Dataset const& d, uint64_t node, int rank, Place& place, int depth = 0) const {
+    if (depth > kMaxDepth) bad("chunk B-tree deeper than " + std::to_string(kMaxDepth));
     if (!sig(node, "TREE")) bad("chunk B-tree node");
     if (buf_[node + 4] != 1) bad("chunk B-tree type");
     const int level = buf_[node + 5];
@@ -668,10 +683,13 @@ class NetCDF4 {
       const uint64_t size = le(p, 4);
       const uint32_t mask = (uint32_t)le(p + 4, 4);
       std::vector<uint64_t> origin(rank);
-      for (int k = 0; k < rank; ++k) origin[k] = le(p + 8 + 8ull * k, 8);
+      for (int k = 0; k < rank; ++k) {
+        origin[k] = le(p + 8 + 8ull * k, 8);
+        if (level == 0 && origin[k] % d.chunk[k]) bad("chunk origin off the chunk grid");
+      }
       const uint64_t child = le(p + key, so_);
       if (level > 0)
-        btree_chunks(d, abs_(child), rank, place);
+        btree_chunks(d, abs_(child), rank, place, depth + 1);
       else
         place(origin, child, size, mask);
       p += key + so_;
