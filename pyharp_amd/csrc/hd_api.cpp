@@ -557,6 +557,15 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
   // `lay` stream beside chunk k's sweep on the caller's stream
   const bool team_pipe = !reg && nsolve > chunk;
   const bool beam = in->fbeam != nullptr;
+  // Register path without Planck emission: the layer kernel's beam sources are for
+  // a unit beam at the layer top and the sweep scales them by exp(-tau_c/mu0) from
+  // its own running depth, so no chunk needs the cumulative-depth prologue -- which
+  // sat on the side stream behind the previous back-substitution and held each
+  // chunk's layer kernel back until the sweep beside it was done.  With Planck the
+  // sources mix beam and thermal terms and the prologue stays.
+  const bool beam_in_sweep = reg && beam && !planck;
+  const bool need_tauc = beam && !beam_in_sweep;
+  const bool need_pro = planck || need_tauc;
   const int nb = 2;  // buffers of the per-chunk regions (two chunks in flight)
   // Scratch regions, sized for the largest chunk so that no region moves between
   // chunks (inside a region the kernels interleave with the chunk's own nsc):
@@ -653,16 +662,16 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
     if (team_pipe) {
       // buffer `buf` is free once sweep k-2 (its last reader) is done
       if (k >= 2) HD_HIP(ctx, hipStreamWaitEvent(ctx->lay, ctx->ev_sweep[buf], 0));
-      hd::launch_prologue(planck ? &pa : nullptr, beam ? &ta : nullptr, ctx->lay);
+      hd::launch_prologue(planck ? &pa : nullptr, need_tauc ? &ta : nullptr, ctx->lay);
     } else if (!reg || single) {
-      hd::launch_prologue(planck ? &pa : nullptr, beam ? &ta : nullptr, stream);
-    } else if (k == 0) {
-      hd::launch_prologue(planck ? &pa : nullptr, beam ? &ta : nullptr, ctx->side);
+      hd::launch_prologue(planck ? &pa : nullptr, need_tauc ? &ta : nullptr, stream);
+    } else if (k == 0 && need_pro) {
+      hd::launch_prologue(planck ? &pa : nullptr, need_tauc ? &ta : nullptr, ctx->side);
       HD_HIP(ctx, hipEventRecord(ctx->ev_pro[0], ctx->side));
     }
     hd::LayerArgs la{};
     la.prop = in->prop;
-    la.tauc = tauc_b[buf];
+    la.tauc = need_tauc ? tauc_b[buf] : nullptr;  // null with a beam: unit beam at the top
     la.fbeam = in->fbeam;
     la.umu0 = in->umu0;
     la.planckv = planck_b[buf];
@@ -700,6 +709,7 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
     sa.sink = ctx->sink;
     sa.cmaj = cmaj;
     sa.nwave = in->nwave;
+    sa.beam_scale = beam_in_sweep ? 1 : 0;
     if (band && reg) {
       sa.wts = band->weight;
       sa.part = part;
@@ -737,7 +747,7 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
     } else if (reg) {
       // layer kernel k on `lay`: its inputs (prologue k) are in, and sweep k-2,
       // the last reader of layer records[buf], is done
-      HD_HIP(ctx, hipStreamWaitEvent(ctx->lay, ctx->ev_pro[buf], 0));
+      if (need_pro) HD_HIP(ctx, hipStreamWaitEvent(ctx->lay, ctx->ev_pro[buf], 0));
       if (k >= 2) HD_HIP(ctx, hipStreamWaitEvent(ctx->lay, ctx->ev_sweep[buf], 0));
       if (ev) HD_HIP(ctx, hipEventRecord(ev[0], ctx->lay));
       e = hd::launch_layer_nn(nn, la, ctx->lay);
@@ -775,11 +785,11 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
       // next chunk's prologue into the other buffer (free: the side stream already
       // waited for the sweep of chunk k-1, the last user of that buffer)
       const long s1 = s0 + chunk;
-      if (s1 < nsolve) {
+      if (s1 < nsolve && need_pro) {
         hd::TaucArgs ta1;
         hd::PlanckArgs pa1;
         prologue_args(s1, (int)std::min(chunk, nsolve - s1), buf ^ 1, ta1, pa1);
-        hd::launch_prologue(planck ? &pa1 : nullptr, beam ? &ta1 : nullptr, ctx->side);
+        hd::launch_prologue(planck ? &pa1 : nullptr, need_tauc ? &ta1 : nullptr, ctx->side);
         HD_HIP(ctx, hipEventRecord(ctx->ev_pro[buf ^ 1], ctx->side));
       }
       HD_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_sweep[buf], 0));

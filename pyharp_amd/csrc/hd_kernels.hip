@@ -370,7 +370,9 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
     for (int i = 0; i < NN; ++i) y[i] = Qc.sd[i] * Qc.mu[i] * sv[i];
     lower_solve<NN>(lch, rdl, y);
     lower_t_solve<NN>(lch, rdl, y);
-    const double tauc = A.tauc[(size_t)lc * A.nsc + sl];  // scaled depth of layer top
+    // scaled depth of the layer top; without the prologue's depths the beam is
+    // taken as unit at the top and the sweep applies exp(-tau_c/mu0)
+    const double tauc = A.tauc ? A.tauc[(size_t)lc * A.nsc + sl] : 0.0;
     const double att = 0.5 * exp(-tauc * rmu0);
 #pragma unroll
     for (int i = 0; i < NN; ++i) {
@@ -561,6 +563,11 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
 #pragma unroll
       for (int i = 0; i < NN; ++i) spl[i] = lp[(size_t)(2 * nsym + i) * nsc];
     }
+    // direct beam at the layer top; the sources of a unit-beam record scale with it
+    const double eb = exp(-tauc * rmu0);
+    const double sscale = A.beam_scale ? eb : 1.0;
+#pragma unroll
+    for (int i = 0; i < NN; ++i) spl[i] *= sscale;
 
     // level lc (top of layer lc): F_dn = rc . I+ + cs
     {
@@ -573,7 +580,7 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
         bp[(size_t)(NN * NN + NN + i) * nsc] = twopi * t;
         cs = fma(Qc.g[i], sd[i], cs);
       }
-      bp[(size_t)(NN * NN + 2 * NN) * nsc] = fma(twopi, cs, f0mu0 * exp(-tauc * rmu0));
+      bp[(size_t)(NN * NN + 2 * NN) * nsc] = fma(twopi, cs, f0mu0 * eb);
     }
     HD_PHASE();
     // A = Ra (full); W1 = I - R_l A ; v1 = R_l Sd + S+
@@ -707,7 +714,7 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
         for (int k = 0; k < NN; ++k) t = fma(HD_SYM(tl, i, k), am[k][j], t);
         ra[i][j] = t;
       }
-      double t = lp[(size_t)(2 * nsym + NN + i) * nsc];
+      double t = lp[(size_t)(2 * nsym + NN + i) * nsc] * sscale;
 #pragma unroll
       for (int k = 0; k < NN; ++k) t = fma(HD_SYM(tl, i, k), u[k], t);
       sd[i] = t;

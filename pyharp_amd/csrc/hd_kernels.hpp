@@ -69,7 +69,7 @@ struct TaucArgs {
 
 struct LayerArgs {
   const double* prop;
-  const double* tauc;     // [nlyr][nsc] (beam) or null
+  const double* tauc;     // [nlyr][nsc] (beam) or null: unit beam at every layer top
   const double* fbeam;
   const double* umu0;
   const double* planckv;  // [nlyr+3][nsc] (planck) or null
@@ -119,6 +119,9 @@ struct SweepArgs {
   int nslot;       // column slots per wave
   int rsteps;      // ceil(log2(min(nwave, 64))) shuffle steps
   int flux_local;  // team path: flux is a chunk buffer [nsc][L+1][2]
+  // register path: the layer records' sources are for a unit beam at each layer
+  // top (LayerArgs.tauc null); the sweep scales them by exp(-tau_c/mu0)
+  int beam_scale;
 };
 
 // chunk epilogue of the fused band sum: bflux[c] (=|+=) sum of the chunk's
