@@ -13,6 +13,12 @@
 
 #include <hip/hip_runtime.h>
 
+// Jacobi rotation angles in FP32 with FP64-normalised c, s (jacobi_os_round,
+// team_jacobi_round); 0: the all-FP64 angle formulas
+#ifndef HD_JACOBI_F32_ANGLE
+#define HD_JACOBI_F32_ANGLE 1
+#endif
+
 namespace hd {
 
 constexpr double kPi = 3.14159265358979323846;
@@ -369,8 +375,22 @@ HD_UNROLL_NN
     const double g2 = gam * gam;
     off += g2;
     const bool rot = on && g2 > 1.0e-30 * (app * aqq);
-    // w = sqrt(d^2 + 4 g^2), u = |d| + w, z = 1/sqrt(2 w u): c = u z, s = sgn(d) 2 g z
     const double d = aqq - app;
+#if HD_JACOBI_F32_ANGLE
+    // The angle in FP32, t = tan(theta) = sgn(d) 2 g / (|d| + sqrt(d^2 + 4 g^2));
+    // c = 1/sqrt(1 + t^2) and s = t c in FP64, so the rotation is orthogonal to FP64
+    // rounding whatever t is: an angle good to ~1e-7 only leaves ~1e-7 of g behind,
+    // which the next sweep removes (quadratic convergence until off ~ 1e-7 of the
+    // diagonal; the stop rule sits at 1e-8)
+    const float df = (float)d, g2f = 2.0f * (float)gam;
+    const float wf = __builtin_amdgcn_sqrtf(__builtin_fmaf(g2f, g2f, df * df));
+    const float tf = (df < 0.0f ? -g2f : g2f) * __builtin_amdgcn_rcpf(__builtin_fabsf(df) + wf);
+    const double t = rot ? (double)tf : 0.0;
+    const double c = rsq_nr1(fma(t, t, 1.0));  // exactly 1 for t = 0
+    cc[k] = c;
+    ss[k] = t * c;
+#else
+    // w = sqrt(d^2 + 4 g^2), u = |d| + w, z = 1/sqrt(2 w u): c = u z, s = sgn(d) 2 g z
     const double w2 = rot ? fma(d, d, 4.0 * g2) : 1.0;
     const double w = w2 * rsq_nr1(w2);
     const double u = fabs(d) + w;
@@ -378,6 +398,7 @@ HD_UNROLL_NN
     const double sg = d < 0.0 ? -2.0 : 2.0;
     cc[k] = rot ? u * z : 1.0;
     ss[k] = rot ? sg * gam * z : 0.0;
+#endif
     gg[k] = gam;
   }
 HD_UNROLL_NN

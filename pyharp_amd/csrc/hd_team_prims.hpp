@@ -262,8 +262,17 @@ __device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double& own, 
   const double g2 = gam * gam, pq = app * aqq;
   const bool r = on && pair && g2 > kJacobiTol2 * pq;
   off += pair ? g2 : 0.0;  // each pair counted by both of its lanes
-  // w = sqrt(d^2 + 4 g^2), u = |d| + w, z = 1/sqrt(2 w u): c = u z, s = sgn(d) 2 g z
   const double d = aqq - app;
+#if HD_JACOBI_F32_ANGLE
+  // the angle in FP32, c and s normalised in FP64 (see jacobi_os_round)
+  const float df = (float)d, g2f = 2.0f * (float)gam;
+  const float wf = __builtin_amdgcn_sqrtf(__builtin_fmaf(g2f, g2f, df * df));
+  const float tf = (df < 0.0f ? -g2f : g2f) * __builtin_amdgcn_rcpf(__builtin_fabsf(df) + wf);
+  const double t = r ? (double)tf : 0.0;
+  const double c = rsq_nr1(fma(t, t, 1.0));  // exactly 1 for t = 0
+  const double s = t * c;
+#else
+  // w = sqrt(d^2 + 4 g^2), u = |d| + w, z = 1/sqrt(2 w u): c = u z, s = sgn(d) 2 g z
   const double w2 = r ? fma(d, d, 4.0 * g2) : 1.0;
   const double w = w2 * rsq_nr1(w2);
   const double u = fabs(d) + w;
@@ -271,6 +280,7 @@ __device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double& own, 
   const double sg = d < 0.0 ? -2.0 : 2.0;
   const double c = r ? u * z : 1.0;
   const double s = r ? sg * gam * z : 0.0;
+#endif
   const double se = lo ? -s : s;  // p side: c b_p - s b_q ; q side: s b_p + c b_q
 #if HD_JACOBI_SCALED
   const double tq = se * sq * rcp_nr(c * sig);
