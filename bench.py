@@ -481,7 +481,8 @@ def main():
                     f"HBM bytes per launch from rocprofv3 PMC run {pmc['source']} "
                     "(2 x FETCH_SIZE + WRITE_SIZE, scaled to this launch's solves); "
                     "algorithmic bytes per solve are much smaller: the layer records "
-                    "(89 doubles per layer) are written to HBM scratch for the sweep",
+                    f"({nstr // 2 * (nstr // 2 + 1) + nstr + 1 if nstr <= 16 else nstr * nstr // 2 + nstr + 2}"
+                    " doubles per layer) are written to HBM scratch for the sweep",
                     "path_bytes_per_solve": path_bytes,
                     "algorithmic_bytes_per_solve": int(nlyr * (2 + nstr) * 8 + 48 + (nlyr + 1) * 16
                                                        + (nlyr + 1) * 8 * int(bool(args.planck))),
