@@ -16,9 +16,12 @@
 // Scratch layout per chunk (solve-interleaved: lane = solve, so every global
 // access of a wave is 64 consecutive doubles):
 //   planck      [L+3][nsc]       B(level 0..L, harp order), B(btemp), temis*B(ttemp)
-//   layer ops   [lc][NE1][nsc]   NE1 = NN(NN+1) + 2NN + 1
-//                                (R~ upper, T~ upper, S~+, S~-, tau')
-//   back-sub    [lc][NE2][nsc]   NE2 = NN^2 + 2NN + 1   (ZT, t, rc, cs)
+//   layer ops   [lc][pair][nsc] double2: RecL (R~ upper, T~ upper, S~+, S~-,
+//                                tau'; 45 pairs at NN = 8)
+//   back-sub    [lc][pair][nsc] double2: RecB (ZT column-major, t, rc, cs; 41
+//                                pairs at NN = 8)
+//   (16 bytes per lane and record access: half the memory instructions, so half
+//   the vmcnt-ordered round trips of the one-wave-per-SIMD sweep)
 #include "hd_kernels.hpp"
 
 namespace hd {
@@ -415,8 +418,9 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
 #pragma unroll
     for (int j = 0; j < NN; ++j) v[i][j] *= dsq[j];
 
-  double* out = A.scr + (size_t)lc * ne1<NN>() * A.nsc + sl;
-  const size_t so = A.nsc;
+  using RL = RecL<NN>;
+  PairOut out{reinterpret_cast<double2*>(A.scr) + (size_t)lc * RL::pairs * A.nsc + sl,
+              (size_t)A.nsc, 0.0};
   constexpr int nsym = NN * (NN + 1) / 2;
   double ga[NN], gb[NN];
 #pragma unroll
@@ -485,24 +489,37 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
 #pragma unroll
     for (int i = 0; i < NN; ++i)
 #pragma unroll
-      for (int j = i; j < NN; ++j) {
+      for (int j = i; j < NN; ++j, ++e) {
         const double r = ap_[i][j] - am_[i][j];
-        const double t = (am_[i][j] + ap_[i][j]) - ((i == j) ? 1.0 : 0.0);
-        out[e * so] = r;
-        out[(nsym + e) * so] = t;
-        chk += r + t;
-        ++e;
+        out.put(RL::R + e, r);
+        chk += r;
       }
+    out.close(RL::R + nsym - 1);
+    e = 0;
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int j = i; j < NN; ++j, ++e) {
+        const double t = (am_[i][j] + ap_[i][j]) - ((i == j) ? 1.0 : 0.0);
+        out.put(RL::T + e, t);
+        chk += t;
+      }
+    out.close(RL::T + nsym - 1);
   }
+  double smv[NN];
 #pragma unroll
   for (int i = 0; i < NN; ++i) {
     const double sp = Qc.g[i] * (zp[i] * (1.0 - e0) - db) + pvec[i] - qvec[i];
-    const double sm = Qc.g[i] * (-zm[i] * (1.0 - e0) + db) - pvec[i] - qvec[i];
-    out[(2 * nsym + i) * so] = sp;
-    out[(2 * nsym + NN + i) * so] = sm;
-    chk += sp + sm;
+    smv[i] = Qc.g[i] * (-zm[i] * (1.0 - e0) + db) - pvec[i] - qvec[i];
+    out.put(RL::Sp + i, sp);
+    chk += sp + smv[i];
   }
-  out[(2 * nsym + 2 * NN) * so] = taup;
+  out.close(RL::Sp + NN - 1);
+#pragma unroll
+  for (int i = 0; i < NN; ++i) out.put(RL::Sm + i, smv[i]);
+  out.close(RL::Sm + NN - 1);
+  out.put(RL::Tau, taup);
+  out.close(RL::Tau);
   if (!isfinite(chk + taup)) st |= kStNonFinite;
   if (st) {
     atomicOr(&A.status[s], st);
@@ -550,8 +567,11 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
   double tauc = 0.0;
 
   for (int lc = 0; lc < L; ++lc) {
-    const double* lp = A.scr + (size_t)lc * ne1<NN>() * nsc + sl;
-    double* bp = A.bsub + (size_t)lc * ne2<NN>() * nsc + sl;
+    using RL = RecL<NN>;
+    using RB = RecB<NN>;
+    const double2* lp = reinterpret_cast<const double2*>(A.scr) + (size_t)lc * RL::pairs * nsc + sl;
+    auto rec = [&](int e) { return pair_get(lp, nsc, e); };
+    PairOut bp{reinterpret_cast<double2*>(A.bsub) + (size_t)lc * RB::pairs * nsc + sl, nsc, 0.0};
     // this layer's R~ (upper) and S~+ ; each record element is read once
     double rl[NN][NN], spl[NN];
     {
@@ -559,9 +579,9 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
 #pragma unroll
       for (int i = 0; i < NN; ++i)
 #pragma unroll
-        for (int j = i; j < NN; ++j) rl[i][j] = lp[(size_t)(e++) * nsc];
+        for (int j = i; j < NN; ++j) rl[i][j] = rec(RL::R + (e++));
 #pragma unroll
-      for (int i = 0; i < NN; ++i) spl[i] = lp[(size_t)(2 * nsym + i) * nsc];
+      for (int i = 0; i < NN; ++i) spl[i] = rec(RL::Sp + i);
     }
     // direct beam at the layer top; the sources of a unit-beam record scale with it
     const double eb = exp(-tauc * rmu0);
@@ -577,10 +597,12 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
         double t = 0.0;
 #pragma unroll
         for (int j = 0; j < NN; ++j) t = fma(HD_SYM(ra, j, i), Qc.g[j], t);
-        bp[(size_t)(NN * NN + NN + i) * nsc] = twopi * t;
+        bp.put(RB::Rc + i, twopi * t);
         cs = fma(Qc.g[i], sd[i], cs);
       }
-      bp[(size_t)(NN * NN + 2 * NN) * nsc] = fma(twopi, cs, f0mu0 * eb);
+      bp.close(RB::Rc + NN - 1);
+      bp.put(RB::Cs, fma(twopi, cs, f0mu0 * eb));
+      bp.close(RB::Cs);
     }
     HD_PHASE();
     // A = Ra (full); W1 = I - R_l A ; v1 = R_l Sd + S+
@@ -639,8 +661,9 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
 #pragma unroll
       for (int k = 0; k < NN; ++k) t = fma(am[i][k], t1[k], t);
       u[i] = t;
-      bp[(size_t)(NN * NN + i) * nsc] = t1[i];
+      bp.put(RB::Tv + i, t1[i]);
     }
+    bp.close(RB::Tv + NN - 1);
     HD_PHASE();
     // M1 = A W1^-1, row-wise in place:  x W1 = a  ->  (x L) U = a
 #pragma unroll
@@ -664,11 +687,11 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
     // T~ (upper), read once; ZT = W1^-1 T_l stored column by column
     double tl[NN][NN];
     {
-      int e = nsym;
+      int e = 0;
 #pragma unroll
       for (int i = 0; i < NN; ++i)
 #pragma unroll
-        for (int j = i; j < NN; ++j) tl[i][j] = lp[(size_t)(e++) * nsc];
+        for (int j = i; j < NN; ++j) tl[i][j] = rec(RL::T + (e++));
     }
 #pragma unroll
     for (int j = 0; j < NN; ++j) {
@@ -685,9 +708,11 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
         for (int k = i + 1; k < NN; ++k) x[i] = fma(-w1[i][k], x[k], x[i]);
         x[i] *= w1[i][i];
       }
+      // ZT column-major: column j is elements j NN .. j NN + NN-1
 #pragma unroll
-      for (int i = 0; i < NN; ++i) bp[(size_t)(i * NN + j) * nsc] = x[i];
+      for (int i = 0; i < NN; ++i) bp.put(RB::Z + j * NN + i, x[i]);
     }
+    bp.close(RB::Z + NN * NN - 1);
     HD_PHASE();
     // P = M1 T_l (row-wise in place)
 #pragma unroll
@@ -714,12 +739,12 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
         for (int k = 0; k < NN; ++k) t = fma(HD_SYM(tl, i, k), am[k][j], t);
         ra[i][j] = t;
       }
-      double t = lp[(size_t)(2 * nsym + NN + i) * nsc] * sscale;
+      double t = rec(RL::Sm + i) * sscale;
 #pragma unroll
       for (int k = 0; k < NN; ++k) t = fma(HD_SYM(tl, i, k), u[k], t);
       sd[i] = t;
     }
-    tauc += lp[(size_t)(2 * nsym + 2 * NN) * nsc];
+    tauc += rec(RL::Tau);
   }
 
   // ---- Lambertian surface: I+ = g x ----
@@ -844,51 +869,54 @@ __device__ __forceinline__ void backsub_body(const SweepArgs& A) {
     const double f0 = A.fsurf[sl], f1 = A.fsurf[nsc + sl];
     emit(0, f0, f1, false);
   }
-  // element e of this layer's record (e = i NN + j: ZT; NN^2 + i: t;
-  // NN^2 + NN + i: rc; NN^2 + 2 NN: cs) through `get`
+  // this layer's record through `get` (RecB element indices: ZT column-major, t,
+  // rc, cs)
+  using RB = RecB<NN>;
   auto layer = [&](int lc, auto&& get) {
     double nip[NN];
 #pragma unroll
     for (int i = 0; i < NN; ++i) {
-      double t = get(NN * NN + i);
+      double t = get(RB::Tv + i);
 #pragma unroll
-      for (int j = 0; j < NN; ++j) t += get(i * NN + j) * ip[j];
+      for (int j = 0; j < NN; ++j) t += get(RB::Z + j * NN + i) * ip[j];
       nip[i] = t;
     }
-    double up = 0.0, dn = get(NN * NN + 2 * NN);
+    double up = 0.0, dn = get(RB::Cs);
 #pragma unroll
     for (int i = 0; i < NN; ++i) {
       ip[i] = nip[i];
       up += Qc.g[i] * nip[i];
-      dn += get(NN * NN + NN + i) * nip[i];
+      dn += get(RB::Rc + i) * nip[i];
     }
     const int lev = L - lc;
     emit(lev, twopi * up, dn, true);
     chk += twopi * up + dn;
   };
-  auto rec_ptr = [&](int lc) { return A.bsub + (size_t)lc * ne2<NN>() * nsc + sl; };
+  auto rec_ptr = [&](int lc) {
+    return reinterpret_cast<const double2*>(A.bsub) + (size_t)lc * RB::pairs * nsc + sl;
+  };
   if constexpr (PRE) {
-    constexpr int NE = NN * NN + 2 * NN + 1;
-    double cur[NE], nxt[NE];
+    constexpr int NP = RB::pairs;
+    double2 cur[NP], nxt[NP];
     {
-      const double* bp = rec_ptr(L - 1);
+      const double2* bp = rec_ptr(L - 1);
 #pragma unroll
-      for (int e = 0; e < NE; ++e) cur[e] = bp[e * nsc];
+      for (int e = 0; e < NP; ++e) cur[e] = bp[e * nsc];
     }
     for (int lc = L - 1; lc >= 0; --lc) {
       if (lc > 0) {
-        const double* bp = rec_ptr(lc - 1);
+        const double2* bp = rec_ptr(lc - 1);
 #pragma unroll
-        for (int e = 0; e < NE; ++e) nxt[e] = bp[e * nsc];
+        for (int e = 0; e < NP; ++e) nxt[e] = bp[e * nsc];
       }
-      layer(lc, [&](int e) { return cur[e]; });
+      layer(lc, [&](int e) { return (e & 1) ? cur[e >> 1].y : cur[e >> 1].x; });
 #pragma unroll
-      for (int e = 0; e < NE; ++e) cur[e] = nxt[e];
+      for (int e = 0; e < NP; ++e) cur[e] = nxt[e];
     }
   } else {
     for (int lc = L - 1; lc >= 0; --lc) {
-      const double* bp = rec_ptr(lc);
-      layer(lc, [&](int e) { return bp[e * nsc]; });
+      const double2* bp = rec_ptr(lc);
+      layer(lc, [&](int e) { return pair_get(bp, nsc, e); });
     }
   }
   if (live && !isfinite(chk)) {
@@ -902,9 +930,12 @@ __device__ __forceinline__ void backsub_body(const SweepArgs& A) {
 // sweep's register file allows one wave per SIMD): a pure stream over the
 // back-substitution records, I+_top = t + ZT I+_bottom, fluxes per level.
 // This one runs on the side stream beside the next chunk's layer kernel, so it
-// must stay small (44 VGPRs: one wave fits next to a layer-kernel wave).
+// must stay small: at most 96 VGPRs (five waves per SIMD), which fit next to a
+// layer-kernel wave as long as that one stays at <= 416 (410 now).  The 16-byte
+// record loads want the registers of a whole pair set in flight (8 waves per SIMD,
+// 64 VGPRs, spilled).
 template <int NN>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5)))
 void hd_backsub_kernel(SweepArgs A) {
   backsub_body<NN, false>(A);
 }
@@ -1107,15 +1138,26 @@ hipError_t launch_sweep_nn(int nn, const SweepArgs& sa, hipStream_t stream) {
   return hipGetLastError();
 }
 
+// register path: records in 16-byte pairs (RecL / RecB), groups padded to even
+static size_t reg_pairs_l(int nn) {
+  const int nsym = nn * (nn + 1) / 2;
+  return (size_t)(2 * even_up(nsym) + 2 * even_up(nn) + 2) / 2;
+}
+static size_t reg_pairs_b(int nn) {
+  return (size_t)(even_up(nn * nn) + 2 * even_up(nn) + 2) / 2;
+}
+
 size_t layer_record_doubles(int nn) {
-  if (nn <= kMaxRegNN) return (size_t)(nn * (nn + 1) + 2 * nn + 1);
+  if (nn <= kMaxRegNN) return 2 * reg_pairs_l(nn);
   return (size_t)(2 * nn * nn + 2 * nn + 2);  // team layout: full R, T rows (+ pad to even)
 }
 
 size_t bsub_record_doubles(int nn) {
-  if (nn <= kMaxRegNN) return (size_t)(nn * nn + 2 * nn + 1);
+  if (nn <= kMaxRegNN) return 2 * reg_pairs_b(nn);
   return (size_t)((nn * nn + 2 * nn + 2) & ~1);
 }
+
+static_assert(RecL<8>::pairs == 45 && RecB<8>::pairs == 41, "C4 record pairs");
 
 size_t scratch_doubles_per_solve(int nn, int nlyr, bool planck) {
   // every per-chunk region is double-buffered: chunk k+1's layer kernel (and its

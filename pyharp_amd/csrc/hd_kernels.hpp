@@ -19,6 +19,48 @@ template <int NN>
 __host__ __device__ constexpr int ne2() {  // per-level back-substitution record
   return NN * NN + 2 * NN + 1;
 }
+// Register-path flux records in 16-byte element pairs: [lc][pair][nsc] of
+// double2, so each lane moves two record elements per memory instruction (a
+// wave's 64 lanes: 1 KB contiguous).  Every group of elements starts at an even
+// element (padded), so a pair never spans two groups.
+__host__ __device__ constexpr int even_up(int n) { return (n + 1) & ~1; }
+template <int NN>
+struct RecL {  // layer record: R~ upper | T~ upper | S~+ | S~- | tau'
+  static constexpr int nsym = NN * (NN + 1) / 2;
+  static constexpr int R = 0;
+  static constexpr int T = R + even_up(nsym);
+  static constexpr int Sp = T + even_up(nsym);
+  static constexpr int Sm = Sp + even_up(NN);
+  static constexpr int Tau = Sm + even_up(NN);
+  static constexpr int pairs = (Tau + 2) / 2;
+};
+template <int NN>
+struct RecB {  // back-substitution record: ZT (column-major) | t | rc | cs
+  static constexpr int Z = 0;
+  static constexpr int Tv = Z + even_up(NN * NN);
+  static constexpr int Rc = Tv + even_up(NN);
+  static constexpr int Cs = Rc + even_up(NN);
+  static constexpr int pairs = (Cs + 2) / 2;
+};
+// writes record elements in increasing order within a group as 16-byte pairs
+struct PairOut {
+  double2* p;
+  size_t stride;  // pairs -> double2 stride (nsc)
+  double pend;
+  __device__ __forceinline__ void put(int e, double v) {
+    if (e & 1) p[(size_t)(e >> 1) * stride] = make_double2(pend, v);
+    else pend = v;
+  }
+  // after the group's last element e: a lone even element goes out with a zero pad
+  __device__ __forceinline__ void close(int e) {
+    if (!(e & 1)) p[(size_t)(e >> 1) * stride] = make_double2(pend, 0.0);
+  }
+};
+__device__ __forceinline__ double pair_get(const double2* p, size_t stride, int e) {
+  const double2 q = p[(size_t)(e >> 1) * stride];
+  return (e & 1) ? q.y : q.x;
+}
+
 // packed row-major upper-triangle index of (i, j) in either order
 template <int NN>
 __host__ __device__ constexpr int sym_index(int i, int j) {
