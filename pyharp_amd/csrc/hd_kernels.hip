@@ -38,6 +38,11 @@ struct QuadTables {
   Quad<8> q8;
 };
 __constant__ QuadTables c_quad;
+// 1/n for the beam's Legendre recursion (uniform index: scalar loads)
+__constant__ double c_inv_int[2 * kMaxRegNN + 2] = {
+    0.0,        1.0,        1.0 / 2,  1.0 / 3,  1.0 / 4,  1.0 / 5,  1.0 / 6,
+    1.0 / 7,    1.0 / 8,    1.0 / 9,  1.0 / 10, 1.0 / 11, 1.0 / 12, 1.0 / 13,
+    1.0 / 14,   1.0 / 15,   1.0 / 16, 1.0 / 17};
 
 template <int NN>
 __device__ __forceinline__ const Quad<NN>& quad() {
@@ -178,9 +183,9 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
       const double ge = (2 * le + 1) * (che - f) * rf;
       const double go = (2 * lo + 1) * (cho - f) * rf;
       const double pe0 = pcur;  // P_le(mu0)
-      const double po0 = ((2 * lo - 1) * mub * pcur - (lo - 1) * pprev) / lo;
+      const double po0 = ((2 * lo - 1) * mub * pcur - (lo - 1) * pprev) * c_inv_int[lo];
       pprev = po0;
-      pcur = ((2 * lo + 1) * mub * po0 - lo * pe0) / (lo + 1);
+      pcur = ((2 * lo + 1) * mub * po0 - lo * pe0) * c_inv_int[lo + 1];
       double ue[NN], uo[NN];
 #pragma unroll
       for (int i = 0; i < NN; ++i) {
@@ -316,7 +321,7 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
 #pragma unroll
     for (int i = 0; i < NN; ++i) k2 = fma(v[i][j], v[i][j], k2);
     if (!(k2 > 0.0)) st |= kStEigen;
-    kk[j] = sqrt(k2 > 0.0 ? k2 : 0.0);
+    kk[j] = k2 > 0.0 ? k2 * rsq_nr1(k2) : 0.0;
   }
 #pragma unroll
   for (int j = 0; j < NN; ++j) {  // U = C^-T B, column by column
@@ -358,7 +363,7 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
         st |= kStResonance;
         den = den < 0.0 ? -1.0e-9 * r2 : 1.0e-9 * r2;
       }
-      tt[j] = t / den;
+      tt[j] = t * rcp_nr(den);
     }
     double sv[NN], y[NN];
 #pragma unroll
@@ -398,8 +403,9 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
     const double m = -expm1(-x);           // 1 - exp(-k tau')
     const double th = m * rcp_nr(2.0 - m);  // tanh(k tau'/2)
     const double delta = x > 1.0e-8 ? th * rcp_nr(kk[j] > 0.0 ? kk[j] : 1.0) : 0.5 * taup;
-    dsq[j] = sqrt(delta);
-    gsq[j] = sqrt(kk[j] * th);
+    const double gg = kk[j] * th;
+    dsq[j] = delta > 0.0 ? delta * rsq_nr1(delta) : 0.0;
+    gsq[j] = gg > 0.0 ? gg * rsq_nr1(gg) : 0.0;
   }
   // Psi^T = L^-T V Gamma^1/2 = L^-T L^-1 U Gamma^1/2 -> LDS (one column per step)
 #pragma unroll
