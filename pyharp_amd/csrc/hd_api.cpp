@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -20,6 +21,7 @@
 #include "../../include/hdharp.h"
 #include "../../include/hdisort.h"
 #include "hd_kernels.hpp"
+#include "hd_team_prims.hpp"
 #include "hd_rad.hpp"
 
 struct hd_context {
@@ -36,6 +38,9 @@ struct hd_context {
   size_t pool_used = 0;
   hd_timing times{};
   int max_sweeps = 16;  // Jacobi sweep cap (debug setter: hd_context_set_max_sweeps)
+  // team-path Jacobi from the tabulated (ssa, chi_1) eigenvectors
+  // (hd_kernels.hpp); HD_JACOBI_WARM=0 in the environment turns it off (A/B)
+  int warm = 1;
   // true while a solve enqueues into a capturing stream: scratch may not grow then
   bool capturing = false;
   std::string err;
@@ -176,6 +181,7 @@ int ensure_tables(hd_context* ctx) {
   const hd::QuadHost* all = quad_host();
   hipError_t e = hd::upload_quad_tables(all);
   if (e == hipSuccess) e = hd::upload_quad_tables_team(all);
+  if (e == hipSuccess) e = hd::upload_warm_tables_team(all);
   if (e != hipSuccess) return fail(ctx, HD_EHIP, "hd_solve: constant upload: %s", hipGetErrorString(e));
   g_tables[ctx->device] = true;
   return HD_OK;
@@ -375,6 +381,7 @@ int hd_context_create(hd_context** out, int device) {
     return fail(nullptr, HD_EINVAL, "hd_context_create: device %d out of range (%d)", device,
                 ndev);
   hd_context* ctx = new hd_context();
+  if (const char* e = std::getenv("HD_JACOBI_WARM")) ctx->warm = std::atoi(e) != 0;
   ctx->device = device;
   auto init = [ctx]() -> int {
     HD_HIP(ctx, hipSetDevice(ctx->device));
@@ -686,6 +693,7 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
     la.nmom = nm;
     la.planck = planck;
     la.max_sweeps = ctx->max_sweeps;
+    la.warm = ctx->warm;
     la.sink = ctx->sink;
     la.cmaj = cmaj;
     la.nwave = in->nwave;

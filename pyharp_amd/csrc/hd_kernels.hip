@@ -22,6 +22,10 @@
 //                                pairs at NN = 8)
 //   (16 bytes per lane and record access: half the memory instructions, so half
 //   the vmcnt-ordered round trips of the one-wave-per-SIMD sweep)
+#include <cmath>
+#include <cstring>
+#include <vector>
+
 #include "hd_kernels.hpp"
 
 namespace hd {
@@ -1021,6 +1025,103 @@ static void fill_quad(Quad<NN>& q, const QuadHost& h) {
     q.rg[i] = 1.0 / h.g[i];
     for (int l = 0; l < 2 * NN; ++l) q.pt[l][i] = h.pt[l][i];
   }
+}
+
+// ---- warm-start eigenvectors of the team Jacobi (hd_kernels.hpp) ----
+namespace {
+typedef long double ld_t;
+// cyclic two-sided Jacobi of the symmetric n x n a; v <- its eigenvectors (columns)
+void host_sym_eig(int n, ld_t (*a)[kMaxNN], ld_t (*v)[kMaxNN]) {
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) v[i][j] = i == j ? 1.0L : 0.0L;
+  for (int sweep = 0; sweep < 64; ++sweep) {
+    ld_t off = 0.0L, dia = 0.0L;
+    for (int i = 0; i < n; ++i) {
+      dia += a[i][i] * a[i][i];
+      for (int j = i + 1; j < n; ++j) off += a[i][j] * a[i][j];
+    }
+    if (!(off > 1.0e-40L * dia)) break;
+    for (int p = 0; p < n; ++p)
+      for (int q = p + 1; q < n; ++q) {
+        const ld_t apq = a[p][q];
+        if (apq == 0.0L) continue;
+        const ld_t th = (a[q][q] - a[p][p]) / (2.0L * apq);
+        const ld_t t = (th >= 0.0L ? 1.0L : -1.0L) / (fabsl(th) + sqrtl(th * th + 1.0L));
+        const ld_t c = 1.0L / sqrtl(t * t + 1.0L), s = t * c;
+        for (int k = 0; k < n; ++k) {  // columns p, q of a and v
+          const ld_t kp = a[k][p], kq = a[k][q];
+          a[k][p] = c * kp - s * kq;
+          a[k][q] = s * kp + c * kq;
+          const ld_t vp = v[k][p], vq = v[k][q];
+          v[k][p] = c * vp - s * vq;
+          v[k][q] = s * vp + c * vq;
+        }
+        for (int k = 0; k < n; ++k) {  // rows p, q of a
+          const ld_t pk = a[p][k], qk = a[q][k];
+          a[p][k] = c * pk - s * qk;
+          a[q][k] = s * pk + c * qk;
+        }
+      }
+  }
+}
+// lower Cholesky factor in place (the upper triangle is zeroed)
+void host_chol(int n, ld_t (*a)[kMaxNN]) {
+  for (int j = 0; j < n; ++j) {
+    ld_t d = a[j][j];
+    for (int k = 0; k < j; ++k) d -= a[j][k] * a[j][k];
+    const ld_t r = sqrtl(d > 0.0L ? d : 1.0e-300L);
+    a[j][j] = r;
+    for (int i = j + 1; i < n; ++i) {
+      ld_t x = a[i][j];
+      for (int k = 0; k < j; ++k) x -= a[i][k] * a[j][k];
+      a[i][j] = x / r;
+      a[j][i] = 0.0L;
+    }
+  }
+}
+}  // namespace
+
+void warm_eigvecs(int nn, const QuadHost& q, int ia, int ib, double* vout) {
+  // the layer kernel's S+ = -A+ and S- = -A- for an HG layer at the bin centre
+  const int N = 2 * nn;
+  const ld_t ssa = (ia + 0.5L) / kWarmG, g = (ib + 0.5L) / kWarmG;
+  const ld_t f = powl(g, (ld_t)N);
+  const ld_t om = ssa * (1.0L - f) / (1.0L - ssa * f), rf = om / (1.0L - f);
+  ld_t sp[kMaxNN][kMaxNN] = {}, sm[kMaxNN][kMaxNN] = {};
+  for (int l = 0; l < N; ++l) {
+    const ld_t gl = (2 * l + 1) * ((l == 0 ? 1.0L : powl(g, (ld_t)l)) - f) * rf;
+    for (int i = 0; i < nn; ++i)
+      for (int k = 0; k < nn; ++k) {
+        const ld_t x = gl * (ld_t)q.pt[l][i] * (ld_t)q.pt[l][k];
+        if (l % 2 == 0) sp[i][k] += x;
+        else sm[i][k] += x;
+      }
+  }
+  for (int i = 0; i < nn; ++i)
+    for (int k = 0; k < nn; ++k) {
+      const ld_t sij = (ld_t)q.sd[i] * (ld_t)q.sd[k];
+      const ld_t dg = i == k ? 1.0L / (ld_t)q.mu[i] : 0.0L;
+      sp[i][k] = dg - sij * sp[i][k];
+      sm[i][k] = dg - sij * sm[i][k];
+    }
+  host_chol(nn, sm);  // L
+  host_chol(nn, sp);  // C
+  ld_t b0[kMaxNN][kMaxNN], sym[kMaxNN][kMaxNN], v[kMaxNN][kMaxNN];
+  for (int i = 0; i < nn; ++i)
+    for (int k = 0; k < nn; ++k) {
+      ld_t t = 0.0L;
+      for (int m = 0; m < nn; ++m) t += sp[m][i] * sm[m][k];  // (C^T L)_ik
+      b0[i][k] = t;
+    }
+  for (int i = 0; i < nn; ++i)
+    for (int k = 0; k < nn; ++k) {
+      ld_t t = 0.0L;
+      for (int m = 0; m < nn; ++m) t += b0[m][i] * b0[m][k];
+      sym[i][k] = t;
+    }
+  host_sym_eig(nn, sym, v);
+  for (int i = 0; i < nn; ++i)
+    for (int j = 0; j < nn; ++j) vout[i * nn + j] = (double)v[i][j];
 }
 
 hipError_t upload_quad_tables(const QuadHost* per_nn /* [kMaxNN], index nn-1 */) {

@@ -129,6 +129,7 @@ struct LayerArgs {
   double* sink;  // team path: store target of lanes >= NN (>= 2*16^2+2*16+2 doubles)
   int cmaj;      // column-major chunk order (solve_of)
   int nwave;
+  int warm;      // team path: start the Jacobi from the (ssa, chi_1) bin's eigenvectors
 };
 
 struct SweepArgs {
@@ -186,6 +187,25 @@ struct QuadHost {
   double mu[kMaxNN], w[kMaxNN], sd[kMaxNN], g[kMaxNN];
   double pt[2 * kMaxNN][kMaxNN];
 };
+
+// Warm start of the team layer kernel's Jacobi (hd_team_mfma.hip, nstr 18..32):
+// for every (ssa, chi_1) bin of a kWarmG x kWarmG grid on [0,1]^2, the
+// eigenvectors V0 of Sym = B0^T B0 of a Henyey-Greenstein layer at the bin
+// centre (B0 = C^T L, the layer kernel's factors).  The kernel runs the Jacobi
+// on B0 V0, whose columns are already close to orthogonal (any orthogonal V0
+// gives the same eigenpairs; the table only saves sweeps: 5 -> 3 per wave at
+// nstr 32, profiles/r03_warm/).  Entry kWarmG^2 is the identity
+// (non-scattering layers: Sym is diagonal).  The register path (nstr <= 16)
+// saves one sweep of four, which does not pay for the rotations
+// (profiles/r03_warm_reg_notkept/).
+constexpr int kWarmG = 16;
+constexpr int kWarmEntries = kWarmG * kWarmG + 1;
+__host__ __device__ constexpr int warm_bin(double x) {
+  // x in [0,1] -> 0..kWarmG-1 (NaN and out-of-range values clamp)
+  return x > 0.0 ? (x < 1.0 ? (int)(x * kWarmG) : kWarmG - 1) : 0;
+}
+// host: the eigenvectors (row-major nn x nn, columns = vectors) of bin (ia, ib)
+void warm_eigvecs(int nn, const QuadHost& q, int ia, int ib, double* v);
 
 // copy the quadrature tables (index nn-1) into the current device's constant memory
 hipError_t upload_quad_tables(const QuadHost* per_nn);       // nn 1..kMaxRegNN

@@ -33,6 +33,7 @@
 // broadcasts, 64-bit selects and register spills were 39% of its VALU
 // instructions at one wave per SIMD (profiles/r02_c5_team_counters_v1.json).
 #include <cmath>
+#include <vector>
 
 #include "hd_rad.hpp"
 #include "hd_team_prims.hpp"
@@ -167,6 +168,16 @@ __device__ __forceinline__ const double* rad_lam(int m) {
   else if constexpr (NN == 14) return &c_rtt.t14.lam[m][0][0];
   else if constexpr (NN == 15) return &c_rtt.t15.lam[m][0][0];
   else return &c_rtt.t16.lam[m][0][0];
+}
+
+// warm-start tables of the team Jacobi (hd_kernels.hpp), every nn 9..16: entry e
+// of nn holds V0 in the M layout, lane (h, c)'s four values V0[h + 4m][c] at
+// (4c + h) * 4 + m (zero beyond nn)
+constexpr int kWarmTeam = 256;
+__device__ double d_warm_team[kMaxNN - kMaxRegNN][kWarmEntries * kWarmTeam];
+template <int NN>
+__device__ __forceinline__ const double* warm_tab_team() {
+  return d_warm_team[NN - kMaxRegNN - 1];
 }
 
 // lane i of each team: column i of the inverse of the lower-triangular J whose
@@ -346,6 +357,42 @@ __global__ __launch_bounds__(64, 2) void hd_team_mfma_layer_kernel(LayerArgs A) 
       bcol[r] = u;
       pin<NN>(ap);
     });
+    // Warm start (hd_kernels.hpp): B0 <- B0 V0 on the matrix core, V0 the
+    // tabulated eigenvectors of each team's (ssa, chi_1) bin (identity for a
+    // non-scattering layer), read straight into the M layout; S1 is free until
+    // C^-T is written to it below
+    if (A.warm) {
+      const double g1 = nm >= 1 ? q[2] : 0.0;
+      const int e = ssa > 0.0 ? warm_bin(ssa) * kWarmG + warm_bin(g1) : kWarmG * kWarmG;
+      int es[4];
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) es[tt] = __builtin_amdgcn_readlane(e, 16 * tt);
+      if (es[0] != kWarmG * kWarmG || es[1] != kWarmG * kWarmG || es[2] != kWarmG * kWarmG ||
+          es[3] != kWarmG * kWarmG) {
+        double X[4][4], V[4][4];
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) {
+          const double2* p = reinterpret_cast<const double2*>(warm_tab_team<NN>() +
+                                                              (size_t)es[tt] * kWarmTeam) +
+                             (c * 4 + h) * 2;
+          const double2 a = p[0], b = p[1];
+          V[tt][0] = a.x;
+          V[tt][1] = a.y;
+          V[tt][2] = b.x;
+          V[tt][3] = b.y;
+        }
+        lds_fence();
+        put_rows<NN>(S1, t, i, bcol);  // tile = B0^T
+        lds_fence();
+        get_m(S1, h, c, X);           // B0^T (M): the A^T operand of B0 V0
+        mprod<false>(X, V, X, h, c);  // B0 V0 (M)
+        lds_fence();
+        put_m(S1, h, c, X);
+        lds_fence();
+        get_cols<NN>(S1, t, i, bcol);  // lane j: column j of B0 V0
+        lds_fence();
+      }
+    }
     double z[NN];
     team_tri_inverse_col<NN>(ap, rdc, z);  // row i of C^-T -> S1
     put_rows<NN>(S1, t, i, z);
@@ -1418,6 +1465,26 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_sweep_kernel(RadArgs A) {
     atomicOr(&A.status[s], st);
     if (st & 0x0F) atomicOr(A.anyerr, 1);
   }
+}
+
+hipError_t upload_warm_tables_team(const QuadHost* per_nn) {
+  std::vector<double> all((size_t)(kMaxNN - kMaxRegNN) * kWarmEntries * kWarmTeam, 0.0);
+  for (int nn = kMaxRegNN + 1; nn <= kMaxNN; ++nn) {
+    double* tab = all.data() + (size_t)(nn - kMaxRegNN - 1) * kWarmEntries * kWarmTeam;
+    for (int e = 0; e < kWarmEntries; ++e) {
+      double v[kMaxNN * kMaxNN];
+      if (e < kWarmG * kWarmG) {
+        warm_eigvecs(nn, per_nn[nn - 1], e / kWarmG, e % kWarmG, v);
+      } else {
+        for (int k = 0; k < nn * nn; ++k) v[k] = k % (nn + 1) == 0 ? 1.0 : 0.0;
+      }
+      double* ent = tab + (size_t)e * kWarmTeam;
+      for (int r = 0; r < nn; ++r)
+        for (int c = 0; c < nn; ++c) ent[(4 * c + r % 4) * 4 + r / 4] = v[r * nn + c];
+    }
+  }
+  return hipMemcpyToSymbol(HIP_SYMBOL(d_warm_team), all.data(), sizeof(double) * all.size(), 0,
+                           hipMemcpyHostToDevice);
 }
 
 hipError_t upload_quad_tables_team_mfma(const QuadTablesTeam& t) {

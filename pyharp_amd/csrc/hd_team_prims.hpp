@@ -44,6 +44,7 @@ void fill_quad_tables_team(const QuadHost* per_nn /* [kMaxNN], index nn-1 */, Qu
 
 // hd_team_mfma.hip: its copy of the team tables, and the MFMA layer kernel
 hipError_t upload_quad_tables_team_mfma(const QuadTablesTeam& t);
+hipError_t upload_warm_tables_team(const QuadHost* per_nn);  // team Jacobi warm start
 hipError_t launch_team_layer_mfma(int nn, const LayerArgs& la, hipStream_t stream);
 hipError_t launch_team_sweep_mfma(int nn, const SweepArgs& sa, hipStream_t stream);
 
