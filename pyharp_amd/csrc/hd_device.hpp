@@ -169,13 +169,17 @@ __device__ inline double plkavg(double wlo, double whi, double t) {
 
 template <int NN>
 __device__ __forceinline__ bool chol_inplace(double (&a)[NN][NN], double (&rd)[NN]) {
-  bool ok = true;
+  // the pivot test is folded into an integer at each step and pinned there: left
+  // as a bool the compiler sinks every `s > 0` to the caller's status update and
+  // keeps the NN pivots live across everything in between
+  int ok = 1;
 HD_UNROLL_NN
   for (int j = 0; j < NN; ++j) {
     double s = a[j][j];
 HD_UNROLL_NN
     for (int k = 0; k < j; ++k) s = fma(-a[j][k], a[j][k], s);
-    ok = ok && (s > 0.0);
+    ok &= s > 0.0 ? 1 : 0;
+    asm volatile("" : "+v"(ok));
     s = s > 1e-300 ? s : 1e-300;
     const double r = rsq_nr(s);
     a[j][j] = s * r;
@@ -188,7 +192,7 @@ HD_UNROLL_NN
       a[i][j] = t * r;
     }
   }
-  return ok;
+  return ok != 0;
 }
 
 // x <- L^-1 x (forward substitution, L lower, rd = 1/diag(L))

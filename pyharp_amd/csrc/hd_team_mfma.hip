@@ -199,6 +199,9 @@ __device__ __forceinline__ void team_tri_inverse_col(double (&jr)[NN], double& j
 // lane i of each team: (X x)_i for X's row i (xr) and x distributed over the team
 template <int NN>
 __device__ __forceinline__ double team_matvec(const double (&xr)[NN], double x) {
+  // x's broadcasts stay here: hoisted to where x is computed they outlive the
+  // phases in between, and the compiler spills all NN of them to scratch
+  pin(x);
   double y = 0.0;
   sfor<0, NN>([&](auto K) { y = fma(xr[HD_K(K)], bc<HD_K(K)>(x), y); });
   return y;

@@ -132,13 +132,17 @@ __device__ __forceinline__ double team_sum(double x) {
 template <int NN, bool WANT_LT>
 __device__ __forceinline__ bool team_chol(double (&a)[NN], double (&lt)[NN], double& rd) {
   const int i = tlane();
-  bool ok = true;
+  // the pivot test is folded into an integer at each step and pinned there: left
+  // as a bool the compiler sinks every `d > 0` to the caller's status update and
+  // keeps all NN pivots live until then (spilled to scratch in the team kernels)
+  int ok = 1;
   rd = 0.0;
   if constexpr (WANT_LT) sfor<0, NN>([&](auto J) { lt[HD_K(J)] = 0.0; });
   sfor<0, NN>([&](auto K) {
     constexpr int k = HD_K(K);
     double d = bc<k>(a[k]);
-    ok = ok && d > 0.0;
+    ok &= d > 0.0 ? 1 : 0;
+    asm volatile("" : "+v"(ok));
     d = d > 1.0e-300 ? d : 1.0e-300;
     const double r = rsq_nr(d);
     const double lkk = d * r;
@@ -157,7 +161,7 @@ __device__ __forceinline__ bool team_chol(double (&a)[NN], double (&lt)[NN], dou
       }
     });
   });
-  return ok;
+  return ok != 0;
 }
 
 // x <- L^-1 x  (x distributed: lane i holds x_i)
