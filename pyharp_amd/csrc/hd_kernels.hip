@@ -642,7 +642,6 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
     for (int k = 0; k < NN; ++k) {
       const double piv = w1[k][k];
       if (!(fabs(piv) > 1.0e-12)) st |= kStPivot;
-      asm volatile("" : "+v"(st));  // the pivot test here, not sunk (cf. chol_inplace)
       const double rp = rcp_nr(piv);
       w1[k][k] = rp;
 #pragma unroll

@@ -687,7 +687,6 @@ __global__ __launch_bounds__(64, 1) void hd_team_mfma_sweep_kernel(SweepArgs A) 
       constexpr int k = HD_K(K);
       const double piv = bc<k>(w[k]);
       if (!(fabs(piv) > 1.0e-12)) st |= kStPivot;
-      asm volatile("" : "+v"(st));  // the pivot test here, not sunk (cf. team_chol)
       const double rp = rcp_nr(piv);
       const double lik = w[k] * rp;
       const double mm = i > k ? lik : 0.0;
