@@ -156,12 +156,30 @@ class DisortImpl : public torch::nn::Cloneable<DisortImpl> {
   explicit DisortImpl(DisortOptions const& op) : options(op) { reset(); }
 
   void reset() override {
+    // cdisort's disort_flag fields as pydisort's flag string names them
+    // (examples/amarsw-ck.yaml:74-90); the semantics match pyharp_amd.disort.check_flags
     static const std::set<std::string> known = {
         "lamber", "quiet", "onlyfl", "planck", "usrtau", "usrang", "intensity_correction",
         "old_intensity_correction", "print-input", "print-fluxes", "print-intensity",
-        "print-transmissivity", "print-phase-function", "deltam", "lyrcut", "ibcnd"};
+        "print-transmissivity", "print-phase-function", "ibcnd", "spher", "general_source",
+        "output_uum"};
     auto flags = parse_flags(options.flags());
     for (auto const& f : flags) TORCH_CHECK(known.count(f), "Disort: unknown flag ", f);
+    // harp's DISORT driver refuses ibcnd (src/rtsolver/rt_solver_disort.cpp_:67-68)
+    TORCH_CHECK(!flags.count("ibcnd"), "RTSolverDisort::CalRadtranFlux: ibcnd = 1, expected 0 "
+                "(the special-case albedo/transmissivity mode is not supported)");
+    TORCH_CHECK(!flags.count("spher"), "Disort: flag 'spher': pseudo-spherical geometry is not "
+                "implemented");
+    TORCH_CHECK(!flags.count("general_source"), "Disort: flag 'general_source': general "
+                "(user-supplied) sources are not implemented");
+    TORCH_CHECK(!flags.count("output_uum"), "Disort: flag 'output_uum': per-mode intensities "
+                "(uum) are not output");
+    TORCH_CHECK(!(flags.count("intensity_correction") && !flags.count("old_intensity_correction") &&
+                  !flags.count("onlyfl")),
+                "Disort: intensity_correction without old_intensity_correction selects cdisort's "
+                "new (Buras-Emde-Dowling) correction, which is not implemented; add "
+                "old_intensity_correction for the Nakajima-Tanaka correction (TMS + IMS) or use "
+                "onlyfl");
     TORCH_CHECK(flags.count("lamber"), "Disort: only Lambertian lower boundaries are supported");
     auto const& ds = options.ds();
     TORCH_CHECK(ds.nstr >= 2 && ds.nstr % 2 == 0 && ds.nstr <= 32,
@@ -174,7 +192,8 @@ class DisortImpl : public torch::nn::Cloneable<DisortImpl> {
                   "Disort: planck needs wave_lower/wave_upper of size nwave");
     onlyfl_ = flags.count("onlyfl") > 0;
     usrtau_ = flags.count("usrtau") > 0;
-    corint_ = flags.count("intensity_correction") + flags.count("old_intensity_correction") > 0;
+    // cdisort corrects with both flags; old_intensity_correction alone applies none
+    corint_ = flags.count("intensity_correction") && flags.count("old_intensity_correction");
     radiance_ = !onlyfl_ || usrtau_;
     rad_ = torch::Tensor();
     auto& d = options.ds();

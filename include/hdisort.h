@@ -21,8 +21,10 @@
  *         (src/index.h:12-18, src/radiation/radiation_band.cpp:116)
  *   bc    per-solve arrays [nwave][ncol] f64 (NULL = default): fbeam (0),
  *         umu0 (1), albedo (0), btemp (0), ttemp (0), temis (0), fisot (0);
- *         umu0 is floored at 1e-3 as harp's driver does
- *         (src/rtsolver/rt_solver_disort.cpp_:80: umu0 = mu > 1e-3 ? mu : 1e-3)
+ *         umu0 is used as given, as pydisort hands it to cdisort: with fbeam > 0
+ *         a umu0 outside (0, 1] is cdisort's input error (c_chekin) and sets
+ *         HD_STATUS_BAD_INPUT (harp's legacy driver floored umu0 at 1e-3 on its
+ *         side, rt_solver_disort.cpp_:80; such a caller clamps umu0 itself)
  *         (src/radiation/radiation_band.hpp:74-77, amars_sw.cpp:276-278,
  *          amars_lw.cpp:73-74)
  *   temf  [ncol][nlyr+1] f64 level temperatures, level 0 = bottom (planck)
@@ -55,6 +57,13 @@ extern "C" {
 
 #define HDISORT_VERSION 100 /* 1.0.0 */
 
+/* Flags of the pydisort flag string (bindings): lamber
+ * (required), onlyfl, planck, usrtau, usrang, intensity_correction +
+ * old_intensity_correction, quiet, print-* are honoured; ibcnd is refused as
+ * harp's driver refuses it (src/rtsolver/rt_solver_disort.cpp_:67-68), and so
+ * are spher, general_source, output_uum and the new intensity correction
+ * (not implemented); unknown names are refused. */
+
 /* return codes */
 #define HD_OK 0
 #define HD_EINVAL 1    /* bad argument / shape / flag                         */
@@ -68,7 +77,8 @@ extern "C" {
 #define HD_FLAG_ONLYFL 0x4u /* fluxes only (always on: the only mode here)    */
 
 /* per-solve status bits (int32 per solve) */
-#define HD_STATUS_BAD_INPUT 0x01 /* tau<0, ssa outside [0,1], f>=1, umu0>1 ... */
+#define HD_STATUS_BAD_INPUT 0x01 /* tau<0, ssa outside [0,1], f>=1, a beam with
+                                    umu0 outside (0,1], albedo outside [0,1] ... */
 #define HD_STATUS_EIGEN 0x02     /* eigenvalue <= 0 / Cholesky breakdown / Jacobi
                                     not converged within the sweep cap          */
 #define HD_STATUS_NONFINITE 0x04 /* NaN/Inf produced                             */
@@ -197,18 +207,21 @@ int hd_solve_band_host(hd_context *ctx, const hd_config *cfg, const hd_inputs *i
  *   phi    HOST [nphi] user azimuths [deg]
  *   phi0   DEVICE [nwave*ncol] beam azimuth [deg] or NULL (0)
  *   onlyfl 1: fluxes at the user depths only (uu untouched)
- *   corint 1: Nakajima-Tanaka correction of the beam radiances (flags
- *          intensity_correction / old_intensity_correction; DISORT 2.0 INTCOR):
+ *   corint 1: Nakajima-Tanaka correction of the beam radiances (cdisort with
+ *          intensity_correction AND old_intensity_correction; DISORT 2.0 INTCOR):
  *          TMS (exact single scattering, STWL eq. 68) plus, for downward
- *          directions, minus the IMS secondary-scattering term (STWL A.13-A.16)
+ *          directions, minus the IMS secondary-scattering term (STWL A.13-A.16);
+ *          0: none.  Any other value is HD_EINVAL: cdisort's new
+ *          (Buras-Emde-Dowling) correction -- intensity_correction without
+ *          old_intensity_correction -- is not implemented, and the bindings
+ *          refuse that flag combination when radiances are requested.
+ * Not capturable into a HIP graph (HD_EINVAL under capture): the user grid is
+ * copied from host arrays.
  * Outputs (device):
  *   flux [nwave][ncol][ntau][2]  index 0 = the deepest user depth (harp order,
  *        as the level fluxes of hd_solve), [..][0] up, [..][1] rfldir + rfldn
  *   uu   [nwave][ncol][nphi][ntau][numu]  radiance, user order
  *        (cdisort's uu[j][lu][iu] per solve)
- * cdisort's new (Buras-Emde-Dowling) correction is not restated: either flag
- * applies the old one (all corrections vanish where the truncation does,
- * chi_nstr = 0).
  */
 typedef struct hd_radiance {
   int ntau;

@@ -258,7 +258,10 @@ def disort_column(dtauc, ssalb, pmom, nstr, *, umu0=1.0, fbeam=0.0,
 
     dtaucp, taucpr, tauc, oprim, gl = setdis(dtauc, ssalb, pmom, nstr)
 
-    beam = fbeam > 0.0 and umu0 > 0.0
+    if fbeam > 0.0 and not (0.0 < umu0 <= 1.0):
+        # cdisort's input check (c_chekin): a beam needs 0 < umu0 <= 1
+        raise ValueError(f"umu0 = {umu0} outside (0, 1] with fbeam > 0")
+    beam = fbeam > 0.0
     if planck:
         pkag = np.array([plkavg(wvnmlo, wvnmhi, t) for t in temper])
         bplanck = plkavg(wvnmlo, wvnmhi, btemp)
@@ -361,16 +364,6 @@ def disort_column(dtauc, ssalb, pmom, nstr, *, umu0=1.0, fbeam=0.0,
 # --------------------------------------------------------------------------- #
 # harp-level driver (pydisort DisortImpl::forward contract)
 # --------------------------------------------------------------------------- #
-UMU0_FLOOR = 1.0e-3
-
-
-def umu0_floor(umu0):
-    """harp's beam cosine: ``ds_.bc.umu0 = ray.mu > 1.E-3 ? ray.mu : 1.E-3``
-    (legacy /root/reference/src/rtsolver/rt_solver_disort.cpp_:80); NaN stays NaN."""
-    u = np.asarray(umu0, np.float64)
-    return np.where(u > UMU0_FLOOR, u, np.where(np.isnan(u), u, UMU0_FLOOR))
-
-
 def disort_forward(prop, bc, temf=None, *, nstr, nmom=None, planck=False,
                    wave_lower=None, wave_upper=None):
     """Batch driver with harp's layout: prop (W, C, L, nprop), layer 0 = bottom.
@@ -390,7 +383,7 @@ def disort_forward(prop, bc, temf=None, *, nstr, nmom=None, planck=False,
             return np.broadcast_to(np.asarray(bc[key], np.float64), (nwave, ncol))
         return np.full((nwave, ncol), default)
 
-    fbeam, umu0, albedo = bcv("fbeam", 0.0), umu0_floor(bcv("umu0", 1.0)), bcv("albedo", 0.0)
+    fbeam, umu0, albedo = bcv("fbeam", 0.0), bcv("umu0", 1.0), bcv("albedo", 0.0)
     btemp, ttemp = bcv("btemp", 0.0), bcv("ttemp", 0.0)
     temis, fisot = bcv("temis", 0.0), bcv("fisot", 0.0)
     flux = np.zeros((nwave, ncol, nlyr + 1, 2))

@@ -328,6 +328,8 @@ static int solve_column(const hdo_column_in *in, double *rfldir, double *rfldn, 
   double cmu[MAXNN], cwt[MAXNN], cmuf[MAXN], cwtf[MAXN];
   double ylm[MAXN][MAXN]; /* ylm[l][i] = P_l(cmuf_i) */
   if (nstr < 2 || nstr % 2 || nn > MAXNN) return 1;
+  /* cdisort's input check (c_chekin): a beam needs 0 < umu0 <= 1 */
+  if (in->fbeam > 0.0 && !(in->umu0 > 0.0 && in->umu0 <= 1.0)) return 1;
   gauss_01(nn, cmu, cwt);
   for (int i = 0; i < nn; ++i) {
     cmuf[i] = cmu[i]; cmuf[nn + i] = -cmu[i];
@@ -622,10 +624,7 @@ long hdo_forward(int nwave, int ncol, int nlyr, int nprop, int nstr, int nmom, i
       hdo_column_in in;
       in.nstr = nstr; in.nlyr = nlyr; in.nmom = nm; in.planck = planck;
       in.dtauc = dtauc; in.ssalb = ssalb; in.pmom = pm; in.temper = tem;
-      /* harp's floor: ds_.bc.umu0 = mu > 1e-3 ? mu : 1e-3
-         (legacy src/rtsolver/rt_solver_disort.cpp_:80); NaN stays NaN */
-      in.umu0 = umu0 ? (umu0[s] > 1.0e-3 ? umu0[s] : (umu0[s] != umu0[s] ? umu0[s] : 1.0e-3))
-                     : 1.0;
+      in.umu0 = umu0 ? umu0[s] : 1.0; /* as given (pydisort passes it to cdisort) */
       in.fbeam = fbeam ? fbeam[s] : 0.0;
       in.albedo = albedo ? albedo[s] : 0.0;
       in.fisot = fisot ? fisot[s] : 0.0;

@@ -57,7 +57,7 @@ import math
 import numpy as np
 import scipy.linalg
 
-from .disort_np import DITHER, double_gauss, legendre_table, plkavg, setdis, soleig, umu0_floor, upisot
+from .disort_np import DITHER, double_gauss, legendre_table, plkavg, setdis, soleig, upisot
 
 
 def lepoly(nstr: int, m: int, mu) -> np.ndarray:
@@ -156,7 +156,10 @@ def disort_rad_column(dtauc, ssalb, pmom, nstr, *, umu, phi, utau, umu0=1.0, phi
     cwt_full = np.concatenate([cwt, cwt])
     dtaucp, taucpr, tauc, oprim, gl = setdis(dtauc, ssalb, pmom, nstr)
     lay, utaupr = _user_taus(utau, dtauc, dtaucp, tauc, taucpr)
-    beam = fbeam > 0.0 and umu0 > 0.0
+    if fbeam > 0.0 and not (0.0 < umu0 <= 1.0):
+        # cdisort's input check (c_chekin): a beam needs 0 < umu0 <= 1
+        raise ValueError(f"umu0 = {umu0} outside (0, 1] with fbeam > 0")
+    beam = fbeam > 0.0
     if planck:
         pkag = np.array([plkavg(wvnmlo, wvnmhi, t) for t in temper])
         bplanck = plkavg(wvnmlo, wvnmhi, btemp)
@@ -498,7 +501,6 @@ def disort_rad_forward(prop, bc, temf=None, *, nstr, umu, phi, utau=None, nmom=N
     keys = dict(fbeam=0.0, umu0=1.0, phi0=0.0, albedo=0.0, btemp=0.0, ttemp=0.0, temis=0.0,
                 fisot=0.0)
     v = {k: bcv(k, d) for k, d in keys.items()}
-    v["umu0"] = umu0_floor(v["umu0"])  # harp's floor (rt_solver_disort.cpp_:80)
     umu = np.atleast_1d(np.asarray(umu, np.float64))
     phi = np.atleast_1d(np.asarray(phi, np.float64))
     flux = uu = None

@@ -1094,6 +1094,11 @@ int validate_rad(hd_context* ctx, const hd_config* cfg, const hd_inputs* in,
   const int ntau = rad->ntau > 0 ? rad->ntau : nlyr + 1;
   const int numu = radiances ? rad->numu : 0;
   const int nphi = radiances ? rad->nphi : 0;
+  if (rad->corint != 0 && rad->corint != 1)
+    return fail(ctx, HD_EINVAL,
+                "hd_solve_radiance: corint=%d; 0 (none) and 1 (Nakajima-Tanaka, cdisort's "
+                "old_intensity_correction) are implemented, cdisort's new correction is not",
+                rad->corint);
   if (rad->ntau < 0 || (rad->ntau > 0 && !rad->utau))
     return fail(ctx, HD_EINVAL, "hd_solve_radiance: ntau=%d needs utau", rad->ntau);
   for (int i = 0; i < rad->ntau; ++i)
@@ -1128,6 +1133,12 @@ int rad_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in,
   const int nm_mode = (radiances && beam) ? cfg->nstr : 1;
   const int nmom = std::max(0, std::min(cfg->nmom, cfg->nprop - 2));
 
+  // the user grid is copied from host arrays and its buffer may grow: a radiance
+  // solve is not capturable (a replay would reread host memory the caller may have
+  // freed, and nothing may be allocated under capture)
+  if (ctx->capturing)
+    return fail(ctx, HD_EINVAL,
+                "hd_solve_radiance: not capturable into a HIP graph (host user grid)");
   rc = ensure_rad_tables(ctx);
   if (rc) return rc;
   // user grid on the device: umu | phi | utau

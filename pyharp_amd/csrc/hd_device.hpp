@@ -25,14 +25,12 @@ constexpr double kPi = 3.14159265358979323846;
 // DISORT 2.0: ssalb == 1 is dithered to 1 - sqrt(10*DBL_EPSILON)
 constexpr double kDither = 4.712160915387242e-08;
 
-// harp's beam-cosine convention (legacy src/rtsolver/rt_solver_disort.cpp_:80,
-// `ds_.bc.umu0 = ray.mu > 1.E-3 ? ray.mu : 1.E-3`): umu0 is floored at 1e-3, so
-// a sun at or below the horizon is a grazing beam (fbeam > 0 still shines).
-// NaN stays NaN (the layer kernels flag it as bad input).
-constexpr double kUmu0Floor = 1.0e-3;
-__host__ __device__ __forceinline__ double umu0_floor(double mu) {
-  return mu > kUmu0Floor ? mu : (mu == mu ? kUmu0Floor : mu);
-}
+// Beam cosine: taken as given, as pydisort's forward passes it to cdisort, whose
+// input check rejects umu0 outside (0, 1] when fbeam > 0 (c_chekin): the layer
+// kernels set HD_STATUS_BAD_INPUT for it (and the beam stays off), so the call
+// fails with HD_ENUMERIC.  harp's legacy driver floored umu0 at 1e-3 on the
+// caller's side before calling cdisort (rt_solver_disort.cpp_:80); a caller that
+// wants that convention clamps its umu0 array itself.
 
 // per-thread status bits (mirrors include/hdisort.h)
 constexpr int kStBadInput = 0x01;

@@ -160,10 +160,10 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
   const double om = ssa * (1.0 - f) / (1.0 - ssa * f);
   const double rf = om / (1.0 - f);
 
-  const double mu0 = A.umu0 ? umu0_floor(A.umu0[s]) : 1.0;
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
   const double fb = A.fbeam ? A.fbeam[s] : 0.0;
   const bool beam = fb > 0.0 && mu0 > 0.0;
-  if (fb > 0.0 && !(mu0 <= 1.0)) st |= kStBadInput;
+  if (fb > 0.0 && !(mu0 > 0.0 && mu0 <= 1.0)) st |= kStBadInput;  // cdisort c_chekin
   const double rmu0 = beam ? 1.0 / mu0 : 0.0;
   const double mub = beam ? mu0 : 0.0;
 
@@ -551,7 +551,7 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
   constexpr int nsym = NN * (NN + 1) / 2;
   int st = 0;
 
-  const double mu0 = A.umu0 ? umu0_floor(A.umu0[s]) : 1.0;
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
   const double fb = A.fbeam ? A.fbeam[s] : 0.0;
   const bool beam = fb > 0.0 && mu0 > 0.0;
   const double alb = A.albedo ? A.albedo[s] : 0.0;

@@ -276,10 +276,10 @@ __global__ __launch_bounds__(kLayerBlockR) void hd_rad_layer_kernel(RadArgs A) {
   const double om = ssa * (1.0 - f) / (1.0 - ssa * f);
   const double rf = om / (1.0 - f);
 
-  const double mu0 = A.umu0 ? umu0_floor(A.umu0[s]) : 1.0;
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
   const double fb = A.fbeam ? A.fbeam[s] : 0.0;
   const bool beam = fb > 0.0 && mu0 > 0.0;
-  if (fb > 0.0 && !(mu0 <= 1.0)) st |= kStBadInput;
+  if (fb > 0.0 && !(mu0 > 0.0 && mu0 <= 1.0)) st |= kStBadInput;  // cdisort c_chekin
   const double rmu0 = beam ? 1.0 / mu0 : 0.0;
   const double mub = beam ? mu0 : 0.0;
   const bool therm = A.planck && m == 0;
@@ -642,7 +642,7 @@ __global__ __launch_bounds__(64) void hd_rad_sweep_kernel(RadArgs A) {
   constexpr int NB = rad_bsub_doubles(NN);
   int st = 0;
 
-  const double mu0 = A.umu0 ? umu0_floor(A.umu0[s]) : 1.0;
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
   const double fb = A.fbeam ? A.fbeam[s] : 0.0;
   const bool beam = fb > 0.0 && mu0 > 0.0;
   double alb = A.albedo ? A.albedo[s] : 0.0;
@@ -921,7 +921,7 @@ __global__ __launch_bounds__(256) void hd_rad_const_kernel(RadArgs A) {
   load_layer<NN>(A, lc, u, lch, rd, v, kk);
   const double* rr = A.rrd + (size_t)lc * rad_rec_doubles(NN) * nu + u;
   const double bt = rr[oBt * nu], slope = rr[(oBt + 1) * nu], taup = rr[(oBt + 2) * nu];
-  const double mu0 = A.umu0 ? umu0_floor(A.umu0[s]) : 1.0;
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
   const double fb = A.fbeam ? A.fbeam[s] : 0.0;
   const double rmu0 = (fb > 0.0 && mu0 > 0.0) ? 1.0 / mu0 : 0.0;
   double cp[NN], cm[NN];
@@ -996,7 +996,7 @@ __global__ __launch_bounds__(256) void hd_rad_flux_kernel(RadArgs A) {
   const double bt = rr[oBt * nu], slope = rr[(oBt + 1) * nu], taup = rr[(oBt + 2) * nu];
   const double scale = tau > 0.0 ? taup / tau : 0.0;
   const double t = fmin(fmax((tu - ttop) * scale, 0.0), taup);
-  const double mu0 = A.umu0 ? umu0_floor(A.umu0[s]) : 1.0;
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
   const double fb = A.fbeam ? A.fbeam[s] : 0.0;
   const bool beam = fb > 0.0 && mu0 > 0.0;
   const double rmu0 = beam ? 1.0 / mu0 : 0.0;
@@ -1072,7 +1072,7 @@ __global__ __launch_bounds__(64) void hd_rad_user_kernel(RadArgs A) {
   const int L = A.nlyr, np = A.nprop, nm = A.nmom;
   const size_t nu = A.nu;
   const double muu = A.umu[iu];
-  const double mu0 = A.umu0 ? umu0_floor(A.umu0[s]) : 1.0;
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
   const double fb = A.fbeam ? A.fbeam[s] : 0.0;
   const bool beam = fb > 0.0 && mu0 > 0.0;
   const double rmu0 = beam ? 1.0 / mu0 : 0.0;
@@ -1408,7 +1408,7 @@ __global__ __launch_bounds__(256) void hd_rad_tms_kernel(RadArgs A, int nstr) {
   const int lu = (int)(r % A.ntau);
   const int j = (int)(r / A.ntau);
   const long s = A.s0 + sl;
-  const double mu0 = A.umu0 ? umu0_floor(A.umu0[s]) : 1.0;
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
   const double fb = A.fbeam ? A.fbeam[s] : 0.0;
   if (!(fb > 0.0 && mu0 > 0.0)) return;
   const int L = A.nlyr, np = A.nprop, nm = A.nmom;

@@ -81,10 +81,10 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_layer_kernel(LayerArgs A) 
   const double om = ssa * (1.0 - f) / (1.0 - ssa * f);
   const double rf = om / (1.0 - f);
 
-  const double mu0 = A.umu0 ? umu0_floor(A.umu0[s]) : 1.0;
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
   const double fb = A.fbeam ? A.fbeam[s] : 0.0;
   const bool beam = fb > 0.0 && mu0 > 0.0;
-  if (fb > 0.0 && !(mu0 <= 1.0)) st |= kStBadInput;
+  if (fb > 0.0 && !(mu0 > 0.0 && mu0 <= 1.0)) st |= kStBadInput;  // cdisort c_chekin
   const double rmu0 = beam ? 1.0 / mu0 : 0.0;
   const double mub = beam ? mu0 : 0.0;
 
@@ -357,7 +357,7 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_sweep_kernel(SweepArgs A) 
   const double msk = act ? 1.0 : 0.0;  // arithmetic lane mask (see the layer kernel)
   const double g_i = Qc.g[ii] * msk;
 
-  const double mu0 = A.umu0 ? umu0_floor(A.umu0[s]) : 1.0;
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
   const double fb = A.fbeam ? A.fbeam[s] : 0.0;
   const bool beam = fb > 0.0 && mu0 > 0.0;
   const double alb = A.albedo ? A.albedo[s] : 0.0;

@@ -265,10 +265,10 @@ __global__ __launch_bounds__(64, 2) void hd_team_mfma_layer_kernel(LayerArgs A) 
   const double om = ssa * (1.0 - f) / (1.0 - ssa * f);
   const double rf = om / (1.0 - f);
 
-  const double mu0 = A.umu0 ? umu0_floor(A.umu0[s]) : 1.0;
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
   const double fb = A.fbeam ? A.fbeam[s] : 0.0;
   const bool beam = fb > 0.0 && mu0 > 0.0;
-  if (fb > 0.0 && !(mu0 <= 1.0)) st |= kStBadInput;
+  if (fb > 0.0 && !(mu0 > 0.0 && mu0 <= 1.0)) st |= kStBadInput;  // cdisort c_chekin
   const double rmu0 = beam ? 1.0 / mu0 : 0.0;
   const double mub = beam ? mu0 : 0.0;
 
@@ -599,7 +599,7 @@ __global__ __launch_bounds__(64, 1) void hd_team_mfma_sweep_kernel(SweepArgs A) 
   for (int k = lane; k < 2 * kSet; k += 64) lds[k] = 0.0;
   lds_fence();
 
-  const double mu0 = A.umu0 ? umu0_floor(A.umu0[s]) : 1.0;
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
   const double fb = A.fbeam ? A.fbeam[s] : 0.0;
   const bool beam = fb > 0.0 && mu0 > 0.0;
   const double alb = A.albedo ? A.albedo[s] : 0.0;
@@ -903,10 +903,10 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_layer_kernel(RadArgs A) {
   const double om = ssa * (1.0 - f) / (1.0 - ssa * f);
   const double rf = om / (1.0 - f);
 
-  const double mu0 = A.umu0 ? umu0_floor(A.umu0[s]) : 1.0;
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
   const double fb = A.fbeam ? A.fbeam[s] : 0.0;
   const bool beam = fb > 0.0 && mu0 > 0.0;
-  if (fb > 0.0 && !(mu0 <= 1.0)) st |= kStBadInput;
+  if (fb > 0.0 && !(mu0 > 0.0 && mu0 <= 1.0)) st |= kStBadInput;  // cdisort c_chekin
   const double rmu0 = beam ? 1.0 / mu0 : 0.0;
   const double mub = beam ? mu0 : 0.0;
   const bool therm = A.planck && m == 0;
@@ -1252,7 +1252,7 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_sweep_kernel(RadArgs A) {
   for (int k = lane; k < 2 * kSet; k += 64) lds[k] = 0.0;
   lds_fence();
 
-  const double mu0 = A.umu0 ? umu0_floor(A.umu0[s]) : 1.0;
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
   const double fb = A.fbeam ? A.fbeam[s] : 0.0;
   const bool beam = fb > 0.0 && mu0 > 0.0;
   double alb = A.albedo ? A.albedo[s] : 0.0;

@@ -39,11 +39,45 @@ from . import _lib
 from .index import IEX, ISS, IPM  # noqa: F401  (re-exported like disort::index)
 from .rtsolver import RTSolver
 
+# cdisort's disort_flag fields as pydisort's flag string names them (the Disort-flags
+# block of examples/amarsw-ck.yaml:74-90, tests/test_disort.cpp:16-18)
 _KNOWN_FLAGS = {
     "lamber", "quiet", "onlyfl", "planck", "usrtau", "usrang", "intensity_correction",
     "old_intensity_correction", "print-input", "print-fluxes", "print-intensity",
-    "print-transmissivity", "print-phase-function", "deltam", "lyrcut", "ibcnd",
+    "print-transmissivity", "print-phase-function", "ibcnd", "spher", "general_source",
+    "output_uum",
 }
+# cdisort flags this solver does not implement: rejected, never silently ignored
+_UNSUPPORTED_FLAGS = {
+    "spher": "pseudo-spherical geometry is not implemented",
+    "general_source": "general (user-supplied) sources are not implemented",
+    "output_uum": "per-mode intensities (uum) are not output",
+}
+
+
+def check_flags(flags: set) -> None:
+    """The flag semantics of the boundary, shared by reset():
+    unknown names raise; ``ibcnd`` raises as harp's DISORT driver does
+    (rt_solver_disort.cpp_:67-68, ``ValueError("RTSolverDisort::CalRadtranFlux",
+    "ibcnd", ds_.flag.ibcnd, 0)``: the albedo/transmissivity mode of cdisort is not
+    harp's); cdisort's new (Buras-Emde-Dowling) intensity correction --
+    ``intensity_correction`` without ``old_intensity_correction`` -- raises when
+    radiances are requested (with ``onlyfl`` cdisort applies no correction, so the
+    flag has no effect there, as in examples/amarsw-ck.yaml:79-82)."""
+    unknown = flags - _KNOWN_FLAGS
+    if unknown:
+        raise RuntimeError(f"Disort: unknown flags {sorted(unknown)}")
+    if "ibcnd" in flags:
+        raise RuntimeError("RTSolverDisort::CalRadtranFlux: ibcnd = 1, expected 0 (the "
+                           "special-case albedo/transmissivity mode is not supported)")
+    for f in sorted(flags & set(_UNSUPPORTED_FLAGS)):
+        raise RuntimeError(f"Disort: flag '{f}': {_UNSUPPORTED_FLAGS[f]}")
+    if ("intensity_correction" in flags and "old_intensity_correction" not in flags
+            and "onlyfl" not in flags):
+        raise RuntimeError("Disort: intensity_correction without old_intensity_correction "
+                           "selects cdisort's new (Buras-Emde-Dowling) correction, which is "
+                           "not implemented; add old_intensity_correction for the "
+                           "Nakajima-Tanaka correction (TMS + IMS) or use onlyfl")
 _BC_KEYS = ("fbeam", "umu0", "albedo", "btemp", "ttemp", "temis", "fisot")
 _BC_IGNORED = ("phi0",)  # azimuth of the beam: used by the radiances only
 
@@ -133,9 +167,7 @@ class Disort(RTSolver):
     def reset(self):
         op = self.options
         flags = op.flag_set()
-        unknown = flags - _KNOWN_FLAGS
-        if unknown:
-            raise RuntimeError(f"Disort: unknown flags {sorted(unknown)}")
+        check_flags(flags)
         ds = op.ds()
         if ds.nstr < 2 or ds.nstr % 2 or ds.nstr > 32:
             raise RuntimeError(f"Disort: nstr={ds.nstr} must be even and in [2, 32]")
@@ -153,9 +185,10 @@ class Disort(RTSolver):
         self.usrtau = "usrtau" in flags
         self.usrang = "usrang" in flags
         self.radiance = (not self.onlyfl) or self.usrtau
-        # Nakajima-Tanaka correction, TMS + IMS (either correction flag; cdisort's
-        # new method is not restated -- DESIGN.md section 8)
-        self.corint = bool(flags & {"intensity_correction", "old_intensity_correction"})
+        # Nakajima-Tanaka correction, TMS + IMS: cdisort applies it with both
+        # intensity_correction and old_intensity_correction; old_intensity_correction
+        # alone applies none (check_flags refuses the new method)
+        self.corint = {"intensity_correction", "old_intensity_correction"} <= flags
         self._rad = None
         if self.radiance:
             if self.usrtau:

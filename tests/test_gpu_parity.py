@@ -518,14 +518,14 @@ def test_full_c4_size_properties(oracle_c):
 
 
 @pytest.mark.parametrize("nstr", [8, 32])
-def test_umu0_floor(oracle_c, nstr):
-    """harp's beam cosine floor, ``umu0 = mu > 1e-3 ? mu : 1e-3`` (legacy
-    /root/reference/src/rtsolver/rt_solver_disort.cpp_:80):
-    umu0 in {-0.5, 0, 1e-4, 1e-3, 2e-3} on the register (nstr 8) and team (nstr 32)
-    kernels against the C oracle, which applies the same floor; the first three
-    equal the 1e-3 solve bit for bit."""
+def test_umu0_as_given(oracle_c, nstr):
+    """umu0 is taken as given, as pydisort passes it to cdisort:
+    tiny positive cosines (1e-4 .. 2e-3) solve like the C oracle on the register
+    (nstr 8) and team (nstr 32) kernels; with fbeam > 0 a cosine outside (0, 1]
+    (cdisort's c_chekin error) sets HD_STATUS_BAD_INPUT on exactly that solve and the
+    synchronous call raises; without a beam umu0 is not looked at."""
     rng = np.random.default_rng(4242 + nstr)
-    u = np.array([-0.5, 0.0, 1e-4, 1e-3, 2e-3])
+    u = np.array([1e-4, 5e-4, 1e-3, 2e-3, 0.7])
     nwave, ncol, nlyr = 2, u.size, 20
     prop, bc, _ = _random_batch(rng, nwave, ncol, nlyr, nstr, False)
     prop[..., 0] = 10.0 ** rng.uniform(-5, -1.5, (nwave, ncol, nlyr))  # the grazing beam survives
@@ -535,9 +535,22 @@ def test_umu0_floor(oracle_c, nstr):
     f = _run(d, prop, bc)
     err = rel_err(f, ref).max()
     assert err < TOL, f"nstr={nstr}: max rel err {err:.3e}"
-    g = _run(d, prop, dict(bc, umu0=np.full((nwave, ncol), 1e-3)))
-    np.testing.assert_array_equal(f[:, :3], g[:, :3])
-    assert np.all(f[:, :, -1, 1] > 0.0)  # the floored beam shines at the top
+    assert np.all(f[:, :, -1, 1] > 0.0)  # the grazing beam shines at the top
+    dev = torch.device("cuda", 0)
+    for bad in (-0.5, 0.0, 1.2, np.nan):
+        ub = bc["umu0"].copy()
+        ub[1, 2] = bad
+        with pytest.raises(RuntimeError):
+            _run(d, prop, dict(bc, umu0=ub))
+        st = torch.zeros(nwave * ncol, dtype=torch.int32, device=dev)
+        _run(d, prop, dict(bc, umu0=ub), status=st)
+        torch.cuda.synchronize()
+        s = st.cpu().numpy().reshape(nwave, ncol)
+        assert s[1, 2] & 0x01 and np.count_nonzero(s & 0x0F) == 1, s
+        fb = bc["fbeam"].copy()
+        fb[1, 2] = 0.0
+        g = _run(d, prop, dict(bc, umu0=ub, fbeam=fb))
+        assert np.all(np.isfinite(g))
 
 
 @pytest.mark.parametrize("nstr", [8, 32])

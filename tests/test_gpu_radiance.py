@@ -316,14 +316,15 @@ def test_ims_aureole_vs_oracle(nstr, monkeypatch):
     assert _col_err(uref, utms) > 1e-4   # the IMS term is resolved by the comparison
 
 
-def test_radiance_umu0_floor():
-    """The intensity path applies harp's umu0 floor (rt_solver_disort.cpp_:80) like
-    the flux path: umu0 in {0, 1e-4, 1e-3, 2e-3} against the radiance oracle."""
+def test_radiance_umu0_as_given():
+    """The intensity path takes umu0 as given like the flux path: tiny positive
+    cosines {1e-4, 5e-4, 1e-3, 2e-3} against the radiance oracle; umu0 = 0 with a
+    beam is cdisort's input error (the call raises)."""
     rng = np.random.default_rng(5150)
     nwave, ncol, nlyr, nstr = 1, 4, 4, 8
     prop, bc, _ = _random_case(rng, nwave, ncol, nlyr, nstr, False)
     prop[..., 0] = 10.0 ** rng.uniform(-4, -2, (nwave, ncol, nlyr))
-    bc["umu0"] = np.array([[0.0, 1e-4, 1e-3, 2e-3]])
+    bc["umu0"] = np.array([[1e-4, 5e-4, 1e-3, 2e-3]])
     total = prop[..., 0].sum(axis=-1).min()
     utau = [0.0, 0.5 * total, total]
     umu = [-1.0, -0.3, 0.2, 0.9]
@@ -335,7 +336,6 @@ def test_radiance_umu0_floor():
     fref, uref = disort_rad_forward(prop, bc, None, nstr=nstr, umu=umu, phi=phi, utau=utau)
     assert _col_err(uu, uref) < TOL, _col_err(uu, uref)
     assert rel_err(flux, fref).max() < TOL
-    bc1 = dict(bc, umu0=np.full((nwave, ncol), 1e-3))
-    d.forward(torch.as_tensor(prop, device=DEV), _dev(bc1))
-    uu1 = d.get_rad().cpu().numpy()
-    np.testing.assert_array_equal(uu[0, :2], uu1[0, :2])  # 0 and 1e-4 solve as 1e-3
+    bc0 = dict(bc, umu0=np.array([[0.5, 0.0, 0.5, 0.5]]))
+    with pytest.raises(RuntimeError):
+        d.forward(torch.as_tensor(prop, device=DEV), _dev(bc0))

@@ -117,6 +117,85 @@ def test_options_validation():
         Disort(op)
 
 
+# (flag string, expected error pattern or None): the boundary's flag semantics
+# (cdisort's flag names, examples/amarsw-ck.yaml:74-90)
+_FLAG_CASES = [
+    ("lamber,quiet,onlyfl", None),
+    ("lamber,quiet,onlyfl,intensity_correction,old_intensity_correction", None),
+    # the BASELINE configs' yaml (amarsw-ck.yaml:79-82): new correction + onlyfl --
+    # cdisort corrects radiances only, so the flux path is unaffected
+    ("lamber,quiet,onlyfl,intensity_correction", None),
+    ("lamber,intensity_correction,old_intensity_correction", None),
+    ("lamber,old_intensity_correction", None),
+    ("lamber,intensity_correction", "Buras-Emde-Dowling"),
+    ("lamber,onlyfl,ibcnd", "ibcnd"),
+    ("lamber,ibcnd", "ibcnd"),
+    ("lamber,onlyfl,spher", "pseudo-spherical"),
+    ("lamber,onlyfl,general_source", "general"),
+    ("lamber,onlyfl,output_uum", "uum"),
+    ("lamber,onlyfl,deltam", "unknown"),
+    ("lamber,onlyfl,lyrcut", "unknown"),
+]
+
+
+@pytest.mark.parametrize("flags,err", _FLAG_CASES)
+def test_flag_semantics(flags, err):
+    """ibcnd is refused as harp's DISORT driver refuses it (rt_solver_disort.cpp_:67-68);
+    spher / general_source / output_uum and cdisort's new intensity correction are not
+    implemented and refused; names cdisort does not have (deltam, lyrcut) are unknown."""
+    from pyharp_amd import Disort, DisortOptions
+    op = DisortOptions().flags(flags).nwave(1).ncol(1)
+    op.ds().nlyr, op.ds().nstr, op.ds().nmom = 4, 8, 8
+    if err is None:
+        Disort(op)
+    else:
+        with pytest.raises(RuntimeError, match=err):
+            Disort(op)
+
+
+def test_correction_flags_select_nakajima_tanaka_only_with_both():
+    from pyharp_amd import Disort, DisortOptions
+
+    def corint(flags):
+        op = DisortOptions().flags(flags).nwave(1).ncol(1)
+        op.ds().nlyr, op.ds().nstr, op.ds().nmom = 4, 8, 8
+        return Disort(op).corint
+
+    assert corint("lamber,intensity_correction,old_intensity_correction")
+    assert not corint("lamber,old_intensity_correction")  # cdisort: no correction
+    assert not corint("lamber")
+
+
+def test_cpp_flag_semantics():
+    """The C++ drop-in (include/harp_amd/disort.hpp) accepts and refuses exactly the
+    flag strings the Python binding does (tests/cpp/flags_check.cpp, no GPU needed)."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(__file__), "cpp", "flags_check")
+    src = exe + ".cpp"
+    hdr = os.path.join(os.path.dirname(__file__), "..", "include", "harp_amd", "disort.hpp")
+    if not os.path.exists(exe) or os.path.getmtime(exe) < max(os.path.getmtime(src),
+                                                              os.path.getmtime(hdr)):
+        torch_dir = os.path.dirname(torch.__file__)
+        root = os.path.join(os.path.dirname(__file__), "..")
+        abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+        subprocess.run(
+            ["/opt/rocm/bin/hipcc", "-O1", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+             "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM", f"-I{root}/include",
+             f"-I{torch_dir}/include", f"-I{torch_dir}/include/torch/csrc/api/include", src,
+             "-o", exe, f"-L{torch_dir}/lib", f"-Wl,-rpath,{torch_dir}/lib", "-ltorch",
+             "-ltorch_cpu", "-lc10", "-ltorch_hip", "-lc10_hip", f"-L{root}/pyharp_amd",
+             "-Wl,-rpath,$ORIGIN/../../pyharp_amd", "-lhdisort", "-lz"],
+            check=True, capture_output=True)
+    out = subprocess.run([exe] + [f for f, _ in _FLAG_CASES], check=True, capture_output=True,
+                         text=True).stdout.strip().split("\n")
+    assert len(out) == len(_FLAG_CASES)
+    for line, (flags, err) in zip(out, _FLAG_CASES):
+        if err is None:
+            assert line == f"OK {flags}", line
+        else:
+            assert line.startswith(f"REJECT {flags}:") and re.search(err, line), line
+
+
 def test_option_accessors_follow_add_arg_idiom():
     from pyharp_amd import DisortOptions
     op = DisortOptions()

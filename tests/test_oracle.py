@@ -142,13 +142,13 @@ def test_layer2level_matches_reference_run():
 
 
 @pytest.mark.parametrize("nstr", [8, 32])
-def test_umu0_floor_in_both_oracles(nstr, oracle_c):
-    """harp's beam cosine floor (legacy src/rtsolver/rt_solver_disort.cpp_:80,
-    ``umu0 = mu > 1e-3 ? mu : 1e-3``): umu0 in {-0.4, 0, 1e-4} solves as 1e-3 in
-    both restatements' batch drivers, 2e-3 does not, and numpy == C."""
+def test_umu0_range_check_in_both_oracles(nstr, oracle_c):
+    """umu0 is taken as given (pydisort passes it to cdisort; no floor): with fbeam > 0
+    a cosine outside (0, 1] is cdisort's input error (c_chekin) in both restatements;
+    without a beam it is not looked at; tiny positive cosines solve, numpy == C."""
     rng = np.random.default_rng(77 + nstr)
     nlyr = 6
-    u = np.array([[-0.4, 0.0, 1e-4, 1e-3, 2e-3]])
+    u = np.array([[1e-4, 1e-3, 2e-3, 1.0]])
     prop = np.zeros((1, u.shape[1], nlyr, 2 + nstr))
     prop[..., 0] = 10.0 ** rng.uniform(-4, -1, (nlyr,))  # thin: the grazing beam survives
     prop[..., 1] = rng.uniform(0.2, 0.95, (nlyr,))
@@ -159,7 +159,15 @@ def test_umu0_floor_in_both_oracles(nstr, oracle_c):
     fc = oracle_c.forward(prop, bc, nstr=nstr)
     fn = disort_np.disort_forward(prop, bc, nstr=nstr)
     assert rel_err(fn, fc).max() < 1e-9
-    for j in range(3):
-        np.testing.assert_array_equal(fc[0, j], fc[0, 3])
-    assert np.abs(fc[0, 4] - fc[0, 3]).max() > 1e-6 * np.abs(fc[0, 3]).max()
-    assert fc[0, 3, -1, 1] > 0.0  # the floored beam still shines at the top
+    assert np.abs(fc[0, 0] - fc[0, 1]).max() > 1e-6 * np.abs(fc[0, 1]).max()
+    assert fc[0, 0, -1, 1] > 0.0  # a grazing beam shines at the top
+    for bad in (-0.4, 0.0, 1.5, np.nan):
+        bb = dict(bc, umu0=np.array([[0.5, bad, 0.5, 0.5]]))
+        with pytest.raises(ArithmeticError):
+            oracle_c.forward(prop, bb, nstr=nstr)
+        with pytest.raises(ValueError):
+            disort_np.disort_forward(prop, bb, nstr=nstr)
+        # no beam: umu0 is not an input of the solve
+        nb = dict(bb, fbeam=np.array([[1.0, 0.0, 1.0, 1.0]]))
+        f0 = oracle_c.forward(prop, nb, nstr=nstr)
+        assert np.all(np.isfinite(f0)) and np.all(f0[0, 1] == 0.0)
