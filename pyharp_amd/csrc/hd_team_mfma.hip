@@ -33,6 +33,7 @@
 // broadcasts, 64-bit selects and register spills were 39% of its VALU
 // instructions at one wave per SIMD (profiles/r02_c5_team_counters_v1.json).
 #include <cmath>
+#include <mutex>
 #include <vector>
 
 #include "hd_rad.hpp"
@@ -1471,21 +1472,27 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_sweep_kernel(RadArgs A) {
 }
 
 hipError_t upload_warm_tables_team(const QuadHost* per_nn) {
-  std::vector<double> all((size_t)(kMaxNN - kMaxRegNN) * kWarmEntries * kWarmTeam, 0.0);
-  for (int nn = kMaxRegNN + 1; nn <= kMaxNN; ++nn) {
-    double* tab = all.data() + (size_t)(nn - kMaxRegNN - 1) * kWarmEntries * kWarmTeam;
-    for (int e = 0; e < kWarmEntries; ++e) {
-      double v[kMaxNN * kMaxNN];
-      if (e < kWarmG * kWarmG) {
-        warm_eigvecs(nn, per_nn[nn - 1], e / kWarmG, e % kWarmG, v);
-      } else {
-        for (int k = 0; k < nn * nn; ++k) v[k] = k % (nn + 1) == 0 ? 1.0 : 0.0;
+  // the host tables (a long-double Jacobi per entry) are built once per process;
+  // each device only receives the copy
+  static std::vector<double> all;
+  static std::once_flag once;
+  std::call_once(once, [per_nn] {
+    all.assign((size_t)(kMaxNN - kMaxRegNN) * kWarmEntries * kWarmTeam, 0.0);
+    for (int nn = kMaxRegNN + 1; nn <= kMaxNN; ++nn) {
+      double* tab = all.data() + (size_t)(nn - kMaxRegNN - 1) * kWarmEntries * kWarmTeam;
+      for (int e = 0; e < kWarmEntries; ++e) {
+        double v[kMaxNN * kMaxNN];
+        if (e < kWarmG * kWarmG) {
+          warm_eigvecs(nn, per_nn[nn - 1], e / kWarmG, e % kWarmG, v);
+        } else {
+          for (int k = 0; k < nn * nn; ++k) v[k] = k % (nn + 1) == 0 ? 1.0 : 0.0;
+        }
+        double* ent = tab + (size_t)e * kWarmTeam;
+        for (int r = 0; r < nn; ++r)
+          for (int c = 0; c < nn; ++c) ent[(4 * c + r % 4) * 4 + r / 4] = v[r * nn + c];
       }
-      double* ent = tab + (size_t)e * kWarmTeam;
-      for (int r = 0; r < nn; ++r)
-        for (int c = 0; c < nn; ++c) ent[(4 * c + r % 4) * 4 + r / 4] = v[r * nn + c];
     }
-  }
+  });
   return hipMemcpyToSymbol(HIP_SYMBOL(d_warm_team), all.data(), sizeof(double) * all.size(), 0,
                            hipMemcpyHostToDevice);
 }

@@ -219,6 +219,16 @@ class H2SO4Simple(_TableAttenuator):
     TYPE = "h2so4_simple"
 
 
+def _check_out(name, out, shape, dev):
+    """A caller-supplied ``out`` is written through its data pointer by the kernel:
+    it must be exactly the contiguous float64 device tensor the kernel assumes."""
+    if (tuple(out.shape) != tuple(shape) or out.dtype != torch.float64
+            or out.device != dev or not out.is_contiguous()):
+        raise RuntimeError(f"{name}: out must be a contiguous float64 tensor of shape "
+                           f"{tuple(shape)} on {dev}, got {tuple(out.shape)} {out.dtype} "
+                           f"on {out.device}")
+
+
 def band_optics(attenuators: Sequence[_TableAttenuator], conc: torch.Tensor, dz: torch.Tensor,
                 kwargs: Dict[str, torch.Tensor], nprop: int = 2,
                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -240,6 +250,7 @@ def band_optics(attenuators: Sequence[_TableAttenuator], conc: torch.Tensor, dz:
     nwave = x.numel()
     if out is None:
         out = torch.empty((nwave, ncol, nlyr, nprop), dtype=torch.float64, device=dev)
+    _check_out("band_optics", out, (nwave, ncol, nlyr, nprop), dev)
     atts = (_lib.HdAttenuator * len(attenuators))(*[a.hd_struct(dev) for a in attenuators])
     lib = _lib.load()
     with torch.cuda.device(dev):
@@ -277,6 +288,7 @@ def band_loop_optics(attenuators: Sequence[_TableAttenuator], conc: torch.Tensor
             raise RuntimeError(f"band_loop_optics: ext0 must hold {(nwave, ncol, nlyr)}")
     if out is None:
         out = torch.empty((nwave, ncol, nlyr, 2 + nmom), dtype=torch.float64, device=dev)
+    _check_out("band_loop_optics", out, (nwave, ncol, nlyr, 2 + nmom), dev)
     structs = []
     for a in attenuators:
         g = a._tables(dev)[3]

@@ -17,7 +17,8 @@
  *   rfm_v0.nc         libver EARLIEST, no creation order: superblock v0, symbol-
  *                     table group, v1 object headers, B-tree v1 chunks, compact
  *   weights_nc4.nc    dimension + variable "weights" (read_weights.cpp:18-46)
- * Values: v(var, i) = sin(0.37 i + var) * 10^((i % 7) - 3) + var, i = C-order index.
+ * Values: v(var, i) = sin(0.37 i + var) * 10^((i % 7) - 3) + var, i = C-order index;
+ * Pressure (var 2): 10^(5 - 0.4 i) * (1 + 0.05 sin(0.37 i + 2)) (positive, decreasing).
  *
  *   gcc make_nc4.c -I/opt/conda/include -L/opt/conda/lib -lhdf5_hl -lhdf5 \
  *       -Wl,-rpath,/opt/conda/lib -lm -o make_nc4 && ./make_nc4 OUTDIR
@@ -34,7 +35,11 @@
 #define NP 11
 #define NT 5
 
-static double val(int var, long i) { return sin(0.37 * i + var) * pow(10.0, (double)(i % 7) - 3.0) + var; }
+/* Pressure (var 2) is a strictly positive, decreasing axis, as RFM.reset takes its log */
+static double val(int var, long i) {
+  if (var == 2) return pow(10.0, 5.0 - 0.4 * (double)i) * (1.0 + 0.05 * sin(0.37 * i + var));
+  return sin(0.37 * i + var) * pow(10.0, (double)(i % 7) - 3.0) + var;
+}
 
 static void check(herr_t e, const char* what) {
   if (e < 0) {

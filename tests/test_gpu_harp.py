@@ -293,3 +293,33 @@ def test_band_loop_optics_bit_identical(nmom, rfm):
                            ext0=None if ext0 is None else torch.as_tensor(ext0, device=DEV))
     ref = H.band_loop_optics(otabs, conc, dz, nmom, wavenumber=wave, ext0=ext0)
     np.testing.assert_array_equal(got.cpu().numpy(), ref)
+
+
+def test_optics_refuse_bad_out():
+    """A caller-supplied ``out`` is written through its pointer by the kernel: a wrong
+    shape, dtype, device or layout is refused before the launch (band_optics and
+    band_loop_optics); a correct one is filled in place."""
+    from pyharp_amd.opacity import band_loop_optics, band_optics
+    s8, h2 = _attenuators()
+    s8.set_asymmetry(0.7)
+    h2.set_asymmetry(0.75)
+    ncol, nlyr, nmom = 2, 5, 4
+    conc = torch.full((ncol, nlyr, 2), 1e-6, dtype=torch.float64, device=DEV)
+    dz = torch.full((ncol, nlyr), 500.0, dtype=torch.float64)
+    kw = {"wavenumber": torch.linspace(2000.0, 40000.0, 3, dtype=torch.float64, device=DEV)}
+    f64 = torch.float64
+    bad = [torch.empty((3, ncol, nlyr, 2 + nmom + 1), dtype=f64, device=DEV),
+           torch.empty((3, ncol, nlyr, 2 + nmom), dtype=torch.float32, device=DEV),
+           torch.empty((3, ncol, nlyr, 2 + nmom), dtype=f64),
+           torch.empty((3, ncol, 2 + nmom, nlyr), dtype=f64, device=DEV).transpose(2, 3)]
+    for out in bad:
+        with pytest.raises(RuntimeError, match="out must be"):
+            band_loop_optics([s8, h2], conc, dz, kw, nmom, out=out)
+        o2 = out[..., :2] if out.dim() == 4 and out.shape[-1] >= 2 else out
+        with pytest.raises(RuntimeError, match="out must be"):
+            band_optics([s8, h2], conc, dz, kw, 2, out=o2 if o2.shape[-1] == 2 else out)
+    good = torch.full((3, ncol, nlyr, 2 + nmom), float("nan"), dtype=f64, device=DEV)
+    ret = band_loop_optics([s8, h2], conc, dz, kw, nmom, out=good)
+    assert ret is good and bool(torch.isfinite(good).all())
+    np.testing.assert_array_equal(good.cpu().numpy(),
+                                  band_loop_optics([s8, h2], conc, dz, kw, nmom).cpu().numpy())

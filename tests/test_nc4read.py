@@ -20,6 +20,7 @@ import subprocess
 
 import numpy as np
 import pytest
+import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FIX = os.path.join(ROOT, "tests", "golden", "nc4")
@@ -36,8 +37,12 @@ EXTRA = {"rfm_nc4.nc": 0, "rfm_nc4_dense.nc": 10, "rfm_nc4_many.nc": 60, "rfm_la
 def expected(var, shape, kind):
     n = int(np.prod(shape))
     # math.sin / math.pow: the C library's, as make_nc4.c computed them
-    v = np.array([math.sin(0.37 * i + var) * math.pow(10.0, (i % 7) - 3.0) + var
-                  for i in range(n)])
+    if var == 2:  # Pressure: positive and decreasing (RFM.reset takes its log)
+        v = np.array([math.pow(10.0, 5.0 - 0.4 * i) * (1.0 + 0.05 * math.sin(0.37 * i + var))
+                      for i in range(n)])
+    else:
+        v = np.array([math.sin(0.37 * i + var) * math.pow(10.0, (i % 7) - 3.0) + var
+                      for i in range(n)])
     if kind == "f4":
         v = v.astype(np.float32).astype(np.float64)
     elif kind == "i4":
@@ -150,6 +155,7 @@ def test_rfm_reset_on_netcdf4_tables(tmp_path, fname):
         tabs[tag] = [RFM(op.copy().species_ids([k]).opacity_files(["ck.nc"])) for k in range(3)]
     for a, b in zip(tabs["nc4"], tabs["classic"]):
         assert a.kshape == b.kshape == (NW, NP, NT)
+        assert bool(torch.isfinite(a.kaxis).all())  # ln p of a positive pressure axis
         for attr in ("kdata", "kaxis", "krefatm"):
             np.testing.assert_array_equal(getattr(a, attr).numpy(), getattr(b, attr).numpy())
 
