@@ -288,6 +288,128 @@ def cpu_baseline(prop, bc, temf, nstr, planck, wl, wu, target_s=10.0, target_1co
             "sample_seconds": round(dt, 2), "sample": sample}, out, count
 
 
+def extra_legs(disort, prop, bc, temf, wts, steps, dev):
+    """SURVEY 8(d)'s companions of the headline (untimed by the driver, rank 0, N = 1):
+      unfused     -- Disort.forward on device tensors (hd_solve: the per-g fluxes stored,
+                     as every reference call site receives them) + hd_band_flux
+      end_to_end  -- Disort.forward on CPU tensors, CPU flux back: pydisort's contract as
+                     the reference calls it (examples/amars_sw.cpp:280, amars_lw.cpp:80,
+                     radiation_band.cpp:124-127) -> hd_solve_host, H2D/D2H included
+      end_to_end_band -- Disort.forward_band on CPU tensors (hd_solve_band_host: only the
+                     band flux comes back)
+    Host arrays are ordinary (pageable) CPU tensors, as the reference's are."""
+    from pyharp_amd.spectral import band_flux
+    W, ncol, nlyr = prop.shape[0], prop.shape[1], prop.shape[2]
+    nsolve = W * ncol
+    out = {}
+    flux = torch.empty((W, ncol, nlyr + 1, 2), dtype=torch.float64, device=dev)
+    band = torch.empty((ncol, nlyr + 1, 2), dtype=torch.float64, device=dev)
+
+    def unfused():
+        disort.forward(prop, bc, temf, out=flux)
+        band_flux(flux, wts, out=band)
+
+    unfused()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        unfused()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    out["unfused"] = {"value": round(nsolve / dt, 1), "unit": "column-solves/s",
+                      "ms_per_step": round(dt * 1e3, 3), "steps": steps,
+                      "entry": "Disort.forward on device tensors (hd_solve, per-g fluxes "
+                               "stored) + hd_band_flux"}
+    del flux
+    hp = prop.cpu()
+    hb = {k: v.cpu() for k, v in bc.items()}
+    ht = None if temf is None else temf.cpu()
+    hw = wts.cpu()
+    host_bytes = int(hp.numel() * 8 + sum(v.numel() * 8 for v in hb.values()) +
+                     (0 if ht is None else ht.numel() * 8))
+    reps = 3
+    for name, call, back in (
+            ("end_to_end", lambda: disort.forward(hp, hb, ht), nsolve * (nlyr + 1) * 16),
+            ("end_to_end_band", lambda: disort.forward_band(hp, hb, ht, weights=hw),
+             ncol * (nlyr + 1) * 16)):
+        r = call()
+        assert r.device.type == "cpu"
+        del r
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            r = call()
+            ts.append(time.perf_counter() - t0)
+            del r
+        dt = sorted(ts)[len(ts) // 2]
+        out[name] = {"value": round(nsolve / dt, 1), "unit": "column-solves/s",
+                     "ms_per_step": round(dt * 1e3, 3), "reps": reps, "timing": "median wall",
+                     "host_bytes_in": host_bytes, "host_bytes_out": int(back),
+                     "entry": ("Disort.forward on CPU tensors -> hd_solve_host (per-g fluxes "
+                               "back to the host)" if name == "end_to_end" else
+                               "Disort.forward_band on CPU tensors -> hd_solve_band_host")}
+    return out
+
+
+def launch_mode(gpus: int, env) -> str:
+    """How this invocation runs (the driver's contract: ``bench.py --gpus N`` alone,
+    or under ``torch.distributed.run`` with N ranks):
+      "single" -- one process, N = 1, no launcher;
+      "rank"   -- one rank of an N-rank job started by a launcher (WORLD_SIZE set);
+      "spawn"  -- --gpus N > 1 without a launcher: this process starts the N ranks.
+    A launcher's WORLD_SIZE that disagrees with --gpus is an error (the line's
+    n_gpus must be the number of ranks that ran)."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus {gpus} must be >= 1")
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {gpus}: run "
+                             "--gpus N under a launcher with N ranks, or --gpus N alone")
+        return "rank"
+    return "spawn" if gpus > 1 else "single"
+
+
+def spawn_ranks(n: int, argv, env=None, program=None) -> int:
+    """Start n fresh rank processes of ``program`` (default: this script with argv) with
+    torch.distributed.run's environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR
+    127.0.0.1, a free MASTER_PORT) and wait for all of them.  This parent never touches
+    the GPU (it only starts children; no exec from a GPU process).  Returns 0 if every
+    rank exited 0, else the first nonzero exit code (a rank killed by a signal counts
+    as 128 + signal); the other ranks are terminated once one has failed."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    base = dict(os.environ if env is None else env)
+    base.update(WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+                MASTER_PORT=str(port))
+    cmd = program if program is not None else [sys.executable, os.path.abspath(__file__)] + \
+        list(argv)
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen(cmd, env=e))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            code = 128 - code if code < 0 else code
+            if code and not rc:
+                rc = code
+                for q in pending:  # a failed rank would leave the others in a collective
+                    q.send_signal(signal.SIGTERM)
+        if pending:
+            time.sleep(0.05)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -304,9 +426,14 @@ def main():
                     help="max solves per internal chunk (hd_context_set_chunk; 0 = auto)")
     ap.add_argument("--no-fuse", action="store_true",
                     help="unfused epilogue: per-g fluxes stored by hd_solve, then hd_band_flux")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the unfused and host-array (end-to-end) legs")
     ap.add_argument("--graph", action="store_true",
                     help="replay the solve + band sum as one captured HIP graph per step")
     args = ap.parse_args()
+    mode = launch_mode(args.gpus, os.environ)
+    if mode == "spawn":
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     cfgd = CONFIGS[args.config]
     for k in ("ncol", "ngpoint", "nlyr", "nstr"):
         if getattr(args, k) is None:
@@ -448,6 +575,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    band_sum = float(band.sum().item())
     nsolve_total = G * ncol
     value = nsolve_total * args.steps / elapsed
     total_flop, k1_flop, k2_flop = algorithmic_flop(nstr, nlyr, args.planck)
@@ -517,6 +645,9 @@ def main():
             bunf = band_flux(flux, wts)
             fused_vs_unfused = float(((band_fused - bunf).abs().max() /
                                       bunf.abs().max()).item())
+        extra = None
+        if world == 1 and not args.no_extra:
+            extra = extra_legs(disort, prop, bc, temf, wts, args.steps, dev)
         if world == 1 and not args.no_cpu_baseline:
             cpu, ref, n = cpu_baseline(prop, bc, temf, nstr, args.planck, wl, wu)
             m = ref.shape[0]
@@ -541,8 +672,14 @@ def main():
                                       ("gloo, rehearsal" if rehearse else "RCCL") + ")") if dist_on
                        else "none"},
             "roofline": roofline, "path_roofline": whole, "cpu_baseline": cpu,
+            "unfused": None if extra is None else extra["unfused"],
+            "end_to_end": None if extra is None else extra["end_to_end"],
+            "end_to_end_band": None if extra is None else extra["end_to_end_band"],
             "max_rel_err_vs_cpu_restatement": max_err,
             "band_fused_vs_unfused_max_rel": fused_vs_unfused,
+            # sum of the (all-reduced) band flux of the last step: equal at every N for a
+            # given workload (tests/test_bench_launch.py, the rehearsal in DESIGN.md 7)
+            "band_flux_sum": band_sum,
         }
         print(json.dumps(line), flush=True)
     if dist_on:

@@ -45,7 +45,7 @@ for step in "$@"; do
       kexpr=""
       [ "${v#*@}" != "$v" ] && kexpr=${v#*@} && kexpr=${kexpr//+/ }
       say "pytest -m gpu $sel ${kexpr:+-k \"$kexpr\"}"
-      timeout -k 10 840 python -u -m pytest $sel -m gpu ${kexpr:+-k "$kexpr"} -x -v --timeout 120 \
+      HD_MARGINS_OUT=$OUT/parity_margins.json timeout -k 10 840 python -u -m pytest $sel -m gpu ${kexpr:+-k "$kexpr"} -x -v --timeout 120 \
         --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || { tail -40 "$OUT/pytest_gpu.log"; exit 1; }
       tail -3 "$OUT/pytest_gpu.log" ;;
     smoke)

@@ -21,3 +21,23 @@ def oracle_c():
     from oracle import oracle_c as oc
     oc.build()
     return oc
+
+
+def pytest_sessionfinish(session, exitstatus):
+    """With HD_MARGINS_OUT set (scripts/gpu.sh does), write every recorded parity
+    margin (tests/helpers.py margin()): per test the largest error and its tolerance
+    ratio, sorted worst first."""
+    out = os.environ.get("HD_MARGINS_OUT")
+    if not out:
+        return
+    import json
+    import helpers
+    worst = {}
+    for node, err in helpers.MARGINS:
+        worst[node] = max(err, worst.get(node, 0.0))
+    rows = sorted(({"test": k, "max_rel_err": v, "tol": helpers.TOL, "frac_of_tol": v / helpers.TOL}
+                   for k, v in worst.items()), key=lambda r: -r["max_rel_err"])
+    os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
+    with open(out, "w") as f:
+        json.dump({"n_tests": len(rows), "n_checks": len(helpers.MARGINS), "worst": rows[:1],
+                   "tests": rows}, f, indent=1)

@@ -14,6 +14,20 @@ FLOOR = 1.0e-6
 TOL = 1.0e-6  # north-star bound: max |dF|/F < 1e-6
 
 
+# Parity margins (tests/conftest.py writes them to $HD_MARGINS_OUT at the end of the
+# session): every GPU-vs-oracle assertion `assert margin(err) < TOL` records its error
+# under the running test's node id, so a speed change that eats tolerance shows up
+# as a number, not only as a pass/fail.
+MARGINS = []
+
+
+def margin(err):
+    err = float(np.max(err))
+    node = os.environ.get("PYTEST_CURRENT_TEST", "?").rsplit(" (", 1)[0]
+    MARGINS.append((node, err))
+    return err
+
+
 def rel_err(f, ref, floor=FLOOR):
     f = np.asarray(f, np.float64)
     ref = np.asarray(ref, np.float64)

@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import TOL, rel_err
+from helpers import TOL, rel_err, margin
 from test_gpu_parity import _disort, _random_batch
 
 pytestmark = pytest.mark.gpu
@@ -75,7 +75,7 @@ def test_band_matches_oracle(oracle_c, nstr, nwave, ncol, planck, chunk):
     w = _dev(wts)
     band = _with_chunk(chunk, lambda: d.forward_band(p, b, t, weights=w)).cpu().numpy()
     err = rel_err(band, bref).max()
-    assert err < TOL, f"fused band vs oracle: {err:.3e}"
+    assert margin(err) < TOL, f"fused band vs oracle: {err:.3e}"
     # unfused GPU path: per-point fluxes, then hd_band_flux
     from pyharp_amd.spectral import band_flux
     flux = d.forward(p, b, t)

@@ -17,7 +17,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import TOL, rel_err
+from helpers import TOL, rel_err, margin
 
 pytestmark = pytest.mark.gpu
 
@@ -108,7 +108,7 @@ def test_two_modules_two_streams(oracle_c, shapes):
     for fa, fb in outs:
         ea = rel_err(fa.cpu().numpy(), ref_a).max()
         eb = rel_err(fb.cpu().numpy(), ref_b).max()
-        assert ea < TOL and eb < TOL, f"stream A {ea:.3e}, stream B {eb:.3e}"
+        assert margin(ea) < TOL and margin(eb) < TOL, f"stream A {ea:.3e}, stream B {eb:.3e}"
 
 
 def test_two_host_threads(oracle_c):
@@ -138,7 +138,7 @@ def test_two_host_threads(oracle_c):
     for i, (nstr, (prop, bc, kw)) in enumerate(cases):
         ref = _oracle(oracle_c, prop, bc, kw, nstr)
         for f in results[i]:
-            assert rel_err(f, ref).max() < TOL
+            assert margin(rel_err(f, ref).max()) < TOL
 
 
 def _swap_inputs(band, nwave, ncol, nlyr, nstr):
@@ -187,4 +187,4 @@ def test_cpp_radiation_band_swap(oracle_c):
         ref = oracle_c.forward(prop, bc, temf, nstr=nstr[b], planck=b == 1,
                                wave_lower=wl, wave_upper=wl + 50.0)
         err = rel_err(got[b], ref).max()
-        assert err < TOL, f"band {b}: max rel err {err:.3e}"
+        assert margin(err) < TOL, f"band {b}: max rel err {err:.3e}"

@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import TOL, rel_err
+from helpers import TOL, rel_err, margin
 from oracle import harp_np as H
 
 pytestmark = pytest.mark.gpu
@@ -130,9 +130,9 @@ def test_amars_sw_end_to_end(oracle_c, nstr):
           "albedo": np.ones((500, 1))}
     fref = oracle_c.forward(r["prop"].cpu().numpy(), bc, nstr=nstr, nmom=nstr)
     f = r["flux"].cpu().numpy()
-    assert rel_err(f, fref).max() < TOL
+    assert margin(rel_err(f, fref).max()) < TOL
     bref = H.band_flux(fref, np.full(500, wave[1] - wave[0]))
-    assert rel_err(r["bflux"].cpu().numpy()[None], bref[None]).max() < TOL
+    assert margin(rel_err(r["bflux"].cpu().numpy()[None], bref[None]).max()) < TOL
     href = H.heating_rate(bref, dz, rho, 844.0)
     h = r["dTdt"].cpu().numpy()
     assert np.abs(h - href).max() <= 1e-6 * np.abs(href).max()
@@ -153,7 +153,7 @@ def test_amars_lw_example(oracle_c):
     ref = oracle_c.forward(prop, bc, temf, nstr=8, planck=True, wave_lower=np.full(16, 1.0),
                            wave_upper=np.full(16, 150.0))
     f = r["flux"].cpu().numpy()
-    assert rel_err(f, ref).max() < TOL
+    assert margin(rel_err(f, ref).max()) < TOL
     assert np.all(np.abs(f[:, 0, -1, 1]) <= 1e-12 * np.abs(f).max())
     np.testing.assert_allclose(f[:, 0, 0, 0], f[:, 0, 0, 1], rtol=1e-12)
     assert r["bflux"].shape == (1, 41, 2)
@@ -180,7 +180,7 @@ def test_cpp_amars_sw(oracle_c, nstr):
           "albedo": np.ones((500, 1))}
     fref = oracle_c.forward(prop, bc, nstr=nstr, nmom=nstr)
     bref = H.band_flux(fref, np.full(500, wave[1] - wave[0]))
-    assert rel_err(lev[None], bref).max() < TOL
+    assert margin(rel_err(lev[None], bref).max()) < TOL
     href = H.heating_rate(bref, dz, rho, 844.0)[0]
     assert np.abs(lay - href).max() <= 1e-6 * np.abs(href).max()
 
@@ -232,10 +232,10 @@ def test_amars_lw_with_rfm_tables(oracle_c, tmp_path):
     bc = {"albedo": np.ones((nw, 1)), "btemp": np.full((nw, 1), 300.0)}
     fref = oracle_c.forward(prop, bc, temf, nstr=8, planck=True, wave_lower=np.full(nw, 1.0),
                             wave_upper=np.full(nw, 150.0))
-    assert rel_err(r["flux"].cpu().numpy(), fref).max() < TOL
+    assert margin(rel_err(r["flux"].cpu().numpy(), fref).max()) < TOL
     np.testing.assert_array_equal(r["weights"].cpu().numpy(), fx["weights"])
     bref = H.band_flux(fref, fx["weights"])
-    assert rel_err(r["bflux"].cpu().numpy()[None], bref[None]).max() < TOL
+    assert margin(rel_err(r["bflux"].cpu().numpy()[None], bref[None]).max()) < TOL
 
 
 def test_cpp_amars_lw(oracle_c, tmp_path):
@@ -263,7 +263,7 @@ def test_cpp_amars_lw(oracle_c, tmp_path):
     fref = oracle_c.forward(prop, bc, np.full((1, 41), 300.0), nstr=8, planck=True,
                             wave_lower=np.full(nw, 1.0), wave_upper=np.full(nw, 150.0))
     bref = H.band_flux(fref, fx["weights"])
-    assert rel_err(bflx[None], bref).max() < TOL
+    assert margin(rel_err(bflx[None], bref).max()) < TOL
 
 
 @pytest.mark.parametrize("nmom", [0, 8, 32])

@@ -11,7 +11,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from helpers import TOL, rel_err
+from helpers import TOL, rel_err, margin
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -90,7 +90,7 @@ def test_solve_host_matches_oracle(hd, oracle_c, nstr, planck):
     assert not (status & 0x0F).any()
     ref = oracle_c.forward(prop, bc, kw.get("temf"), nstr=nstr, planck=planck,
                            wave_lower=kw.get("wl"), wave_upper=kw.get("wu"))
-    assert rel_err(flux, ref).max() < TOL
+    assert margin(rel_err(flux, ref).max()) < TOL
 
 
 @pytest.mark.parametrize("nstr,keep", [(16, True), (16, False), (32, False)])
@@ -105,9 +105,9 @@ def test_solve_band_host_matches_oracle(hd, oracle_c, nstr, keep):
     ref = oracle_c.forward(prop, bc, nstr=nstr)
     bref = (ref * w[:, None, None, None]).sum(axis=0)
     scale = np.abs(bref).max()
-    assert (np.abs(bflux - bref) / np.maximum(np.abs(bref), 1e-6 * scale)).max() < TOL
+    assert margin((np.abs(bflux - bref) / np.maximum(np.abs(bref), 1e-6 * scale)).max()) < TOL
     if keep:
-        assert rel_err(flux, ref).max() < TOL
+        assert margin(rel_err(flux, ref).max()) < TOL
 
 
 @pytest.mark.parametrize("band", [False, True])
@@ -128,7 +128,7 @@ def test_host_pieces_pipeline(hd, oracle_c, band):
     for q in idx:
         oracle_c.forward(prop, bc, nstr=nstr, first=int(q), count=1, out=ref)
     got = flux.reshape(-1, nlyr + 1, 2)[idx]
-    assert rel_err(got, ref.reshape(-1, nlyr + 1, 2)[idx]).max() < TOL
+    assert margin(rel_err(got, ref.reshape(-1, nlyr + 1, 2)[idx]).max()) < TOL
     if band:
         cols = rng.choice(ncol, 20, replace=False)
         sub = {k: v[:, cols] for k, v in bc.items()}
@@ -178,6 +178,6 @@ def test_plain_c_caller(oracle_c):
                 prop[w, c, l, 1] = 0.3 + 0.05 * ((3 * l + w) % 13)
                 prop[w, c, l, 2:] = g ** np.arange(1, NSTR + 1)
     ref = oracle_c.forward(prop, bc, nstr=NSTR)
-    assert rel_err(flux, ref).max() < TOL
+    assert margin(rel_err(flux, ref).max()) < TOL
     bref = (ref * np.array([0.2, 0.3, 0.5])[:, None, None, None]).sum(axis=0)
     assert np.abs(band - bref).max() <= 1e-9 * np.abs(bref).max()

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import TOL, case_bc, disotest, load_cases, rel_err
+from helpers import TOL, case_bc, disotest, load_cases, rel_err, margin
 
 pytestmark = pytest.mark.gpu
 
@@ -71,7 +71,7 @@ def test_golden_cases(name):
                   wl=d.get("wave_lower"), wu=d.get("wave_upper"))
     f = _run(dis, prop, case_bc(d), d.get("temf"))
     err = rel_err(f, d["flux"]).max()
-    assert err < TOL, f"{name}: max rel err {err:.3e}"
+    assert margin(err) < TOL, f"{name}: max rel err {err:.3e}"
 
 
 def _random_batch(rng, nwave, ncol, nlyr, nstr, planck, beam=True, ssa_max=0.99, gmax=0.85):
@@ -109,7 +109,7 @@ def test_vs_c_oracle(oracle_c, nstr, planck):
                 wu=kw.get("wave_upper"))
     f = _run(d, prop, bc, kw.get("temf"))
     err = rel_err(f, ref).max()
-    assert err < TOL, f"nstr={nstr} planck={planck}: max rel err {err:.3e}"
+    assert margin(err) < TOL, f"nstr={nstr} planck={planck}: max rel err {err:.3e}"
 
 
 def test_headline_config_subsample(oracle_c):
@@ -126,7 +126,7 @@ def test_headline_config_subsample(oracle_c):
     fw = f.reshape(-1, nlyr + 1, 2)[idx]
     rw = ref.reshape(-1, nlyr + 1, 2)[idx]
     err = rel_err(fw, rw).max()
-    assert err < TOL, f"max rel err {err:.3e}"
+    assert margin(err) < TOL, f"max rel err {err:.3e}"
 
 
 def test_aerosol_config_subsample(oracle_c):
@@ -150,7 +150,28 @@ def test_aerosol_config_subsample(oracle_c):
     for s in idx:
         oracle_c.forward(prop, bc, nstr=nstr, first=int(s), count=1, out=ref)
     err = rel_err(f.reshape(-1, nlyr + 1, 2)[idx], ref.reshape(-1, nlyr + 1, 2)[idx]).max()
-    assert err < TOL, f"max rel err {err:.3e}"
+    assert margin(err) < TOL, f"max rel err {err:.3e}"
+
+
+def test_bench_c5_workload_slab(oracle_c):
+    """The exact ``bench.py --config c5`` workload (make_aerosol_inputs: band-loop S8 +
+    H2SO4 optics from the reference's tables, nstr 32, nlyr 80, all 1000 columns) for 8
+    of its 64 spectral points, solved on the team/MFMA path as the bench solves it; a
+    512-solve slab (the first 64 columns of each point) against the C oracle."""
+    import bench
+    dev = torch.device("cuda", 0)
+    gpts = list(range(0, 64, 9))  # 0, 9, ..., 63
+    ncol, nlyr, nstr = 1000, 80, 32
+    prop, bc, _ = bench.make_aerosol_inputs(gpts, 64, ncol, nlyr, nstr, dev)
+    d = _disort(nstr, nlyr, len(gpts), ncol)
+    f = d.forward(prop, bc).cpu().numpy()
+    pn = prop.cpu().numpy()
+    bn = {k: v.cpu().numpy() for k, v in bc.items()}
+    ref = np.zeros_like(f)
+    for i in range(len(gpts)):
+        oracle_c.forward(pn, bn, nstr=nstr, first=i * ncol, count=64, out=ref)
+    err = rel_err(f[:, :64], ref[:, :64]).max()
+    assert margin(err) < TOL, f"max rel err {err:.3e}"
 
 
 @pytest.mark.parametrize("nstr,planck", [(8, False), (24, False), (24, True), (32, True)])
@@ -209,7 +230,7 @@ def test_chunk_sizes_with_partial_waves(oracle_c, nstr, planck):
     assert np.array_equal(out[130], out[17])
     ref = oracle_c.forward(prop, bc, kw.get("temf"), nstr=nstr, planck=planck,
                            wave_lower=kw.get("wave_lower"), wave_upper=kw.get("wave_upper"))
-    assert rel_err(out[0], ref).max() < TOL
+    assert margin(rel_err(out[0], ref).max()) < TOL
 
 
 def test_linearity_in_fbeam():
@@ -255,7 +276,7 @@ def test_edge_cases(oracle_c):
           "albedo": np.array([[0.0, 1.0, 0.5, 0.2, 0.3, 0.0]])}
     ref = oracle_c.forward(prop, bc, nstr=nstr)
     f = _run(_disort(nstr, nlyr, 1, 6), prop, bc)
-    assert rel_err(f, ref).max() < TOL
+    assert margin(rel_err(f, ref).max()) < TOL
     # transparent column: F_dn = mu0 F0 everywhere, F_up = albedo * mu0 F0 = 0
     assert np.allclose(f[0, 0, :, 1], 1.0, rtol=1e-14)
 
@@ -296,7 +317,7 @@ def test_cpu_tensors_round_trip(oracle_c):
     out = d.forward(torch.as_tensor(prop), {k: torch.as_tensor(v) for k, v in bc.items()})
     assert out.device.type == "cpu"
     ref = oracle_c.forward(prop, bc, nstr=4)
-    assert rel_err(out.numpy(), ref).max() < TOL
+    assert margin(rel_err(out.numpy(), ref).max()) < TOL
 
 
 @pytest.mark.parametrize("planck", [False, True])
@@ -314,7 +335,7 @@ def test_cpu_tensors_band_and_planck(oracle_c, planck):
     ref = oracle_c.forward(prop, bc, kw.get("temf"), nstr=nstr, planck=planck,
                            wave_lower=kw.get("wave_lower"), wave_upper=kw.get("wave_upper"))
     f = d.forward(pt, bt, tt)
-    assert f.device.type == "cpu" and rel_err(f.numpy(), ref).max() < TOL
+    assert margin(f.device.type == "cpu" and margin(rel_err(f.numpy(), ref).max())) < TOL
     w = rng.uniform(0.1, 1.0, nwave)
     b = d.forward_band(pt, bt, tt, weights=torch.as_tensor(w))
     assert b.device.type == "cpu"
@@ -351,9 +372,9 @@ def test_cpp_dropin(oracle_c):
     bc = {"fbeam": np.ones((nwave, ncol)), "umu0": np.ones((nwave, ncol)),
           "albedo": np.ones((nwave, ncol))}
     ref = oracle_c.forward(prop, bc, nstr=nstr)
-    assert rel_err(got, ref).max() < TOL
+    assert margin(rel_err(got, ref).max()) < TOL
     bref = np.einsum("w,wclk->clk", 1.0 + 0.1 * np.arange(nwave), ref)
-    assert rel_err(band, bref).max() < TOL
+    assert margin(rel_err(band, bref).max()) < TOL
 
 
 def _lw_problem(G, nstr, nlyr, tau, band, ck, seed=20250217):
@@ -380,7 +401,7 @@ def test_c1_amars_lw_shape(oracle_c, nstr):
     d = _disort(nstr, 40, 16, 1, planck=True, wl=wl, wu=wu)
     f = _run(d, prop, bc, temf)
     ref = oracle_c.forward(prop, bc, temf, nstr=nstr, planck=True, wave_lower=wl, wave_upper=wu)
-    assert rel_err(f, ref).max() < TOL
+    assert margin(rel_err(f, ref).max()) < TOL
 
 
 def test_c3_line_by_line_shape(oracle_c):
@@ -391,7 +412,7 @@ def test_c3_line_by_line_shape(oracle_c):
     d = _disort(8, 40, G, 1, planck=True, wl=wl, wu=wu)
     f = _run(d, prop, bc, temf)
     ref = oracle_c.forward(prop, bc, temf, nstr=8, planck=True, wave_lower=wl, wave_upper=wu)
-    assert rel_err(f, ref).max() < TOL
+    assert margin(rel_err(f, ref).max()) < TOL
 
 
 def test_c3_line_by_line_1e5(oracle_c):
@@ -403,7 +424,7 @@ def test_c3_line_by_line_1e5(oracle_c):
     d = _disort(8, 40, G, 1, planck=True, wl=wl, wu=wu)
     f = _run(d, prop, bc, temf)
     ref = oracle_c.forward(prop, bc, temf, nstr=8, planck=True, wave_lower=wl, wave_upper=wu)
-    assert rel_err(f, ref).max() < TOL
+    assert margin(rel_err(f, ref).max()) < TOL
 
 
 @pytest.mark.parametrize("nstr", [8, 32])
@@ -479,7 +500,7 @@ def test_planck_edge_cases(oracle_c, nstr):
     ref = oracle_c.forward(prop, bc, temf, nstr=nstr, planck=True, wave_lower=wl, wave_upper=wu)
     d = _disort(nstr, nlyr, 1, 6, planck=True, wl=wl, wu=wu)
     f = _run(d, prop, bc, temf)
-    assert rel_err(f, ref).max() < TOL
+    assert margin(rel_err(f, ref).max()) < TOL
 
 
 def test_full_c4_size_properties(oracle_c):
@@ -514,7 +535,7 @@ def test_full_c4_size_properties(oracle_c):
     for q in idx:
         oracle_c.forward(pn, bn, nstr=nstr, first=int(q), count=1, out=ref)
     got = f.cpu().numpy().reshape(-1, L + 1, 2)[idx]
-    assert rel_err(got, ref.reshape(-1, L + 1, 2)[idx]).max() < TOL
+    assert margin(rel_err(got, ref.reshape(-1, L + 1, 2)[idx]).max()) < TOL
 
 
 @pytest.mark.parametrize("nstr", [8, 32])
@@ -534,7 +555,7 @@ def test_umu0_as_given(oracle_c, nstr):
     d = _disort(nstr, nlyr, nwave, ncol)
     f = _run(d, prop, bc)
     err = rel_err(f, ref).max()
-    assert err < TOL, f"nstr={nstr}: max rel err {err:.3e}"
+    assert margin(err) < TOL, f"nstr={nstr}: max rel err {err:.3e}"
     assert np.all(f[:, :, -1, 1] > 0.0)  # the grazing beam shines at the top
     dev = torch.device("cuda", 0)
     for bad in (-0.5, 0.0, 1.2, np.nan):

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import TOL, disotest, rel_err
+from helpers import TOL, disotest, rel_err, margin
 from oracle.disort_rad_np import disort_rad_forward
 
 pytestmark = pytest.mark.gpu
@@ -126,8 +126,8 @@ def test_radiances_vs_oracle(nstr, planck):
                                     utau=utau, planck=planck, wave_lower=kw.get("wave_lower"),
                                     wave_upper=kw.get("wave_upper"))
     assert uu.shape == uref.shape
-    assert _col_err(uu, uref) < TOL, _col_err(uu, uref)
-    assert rel_err(flux, fref).max() < TOL
+    assert margin(_col_err(uu, uref)) < TOL, _col_err(uu, uref)
+    assert margin(rel_err(flux, fref).max()) < TOL
 
 
 @pytest.mark.parametrize("numu", [8, 9, 16])
@@ -152,8 +152,8 @@ def test_radiances_many_angles_vs_oracle(numu, nstr, planck):
                                     utau=utau, planck=planck, wave_lower=kw.get("wave_lower"),
                                     wave_upper=kw.get("wave_upper"))
     assert uu.shape == uref.shape
-    assert _col_err(uu, uref) < TOL, _col_err(uu, uref)
-    assert rel_err(flux, fref).max() < TOL
+    assert margin(_col_err(uu, uref)) < TOL, _col_err(uu, uref)
+    assert margin(rel_err(flux, fref).max()) < TOL
 
 
 def test_rayleigh_nonuniform_azimuth_vs_oracle():
@@ -167,8 +167,8 @@ def test_rayleigh_nonuniform_azimuth_vs_oracle():
     uu = d.get_rad().cpu().numpy()
     fref, uref = disort_rad_forward(prop, bc, nstr=8, umu=umu, phi=phi)
     assert uu.shape == (2, 2, 7, 6, 4)
-    assert _col_err(uu, uref) < TOL
-    assert rel_err(flux, fref).max() < TOL
+    assert margin(_col_err(uu, uref)) < TOL
+    assert margin(rel_err(flux, fref).max()) < TOL
     assert np.abs(uu[:, :, 0] - uu[:, :, -1]).max() > 1e-3 * np.abs(uu).max()
 
 
@@ -197,7 +197,7 @@ def test_onlyfl_user_depths_vs_oracle():
     flux = d.forward(torch.as_tensor(prop, device=DEV), _dev(bc)).cpu().numpy()
     fref, _ = disort_rad_forward(prop, bc, nstr=8, umu=[0.5], phi=[0.0], utau=utau, onlyfl=True)
     assert flux.shape == (2, 2, 9, 2)
-    assert rel_err(flux, fref).max() < TOL
+    assert margin(rel_err(flux, fref).max()) < TOL
     with pytest.raises(RuntimeError):
         d.get_rad()
 
@@ -278,7 +278,7 @@ def test_tms_corrected_radiances_vs_oracle(nstr):
     _, uref = disort_rad_forward(prop, bc, nstr=nstr, nmom=nmom, umu=umu, phi=phi, utau=utau,
                                  corint=True)
     _, u0 = disort_rad_forward(prop, bc, nstr=nstr, nmom=nmom, umu=umu, phi=phi, utau=utau)
-    assert _col_err(uu, uref) < TOL
+    assert margin(_col_err(uu, uref)) < TOL
     assert _col_err(uref, u0) > 1e-3   # the correction is not a no-op here
 
 
@@ -309,7 +309,7 @@ def test_ims_aureole_vs_oracle(nstr, monkeypatch):
     uu = d.get_rad().cpu().numpy()
     _, uref = disort_rad_forward(prop, bc, nstr=nstr, nmom=nmom, umu=umu, phi=phi, utau=utau,
                                  corint=True)
-    assert _col_err(uu, uref) < TOL
+    assert margin(_col_err(uu, uref)) < TOL
     monkeypatch.setattr(disort_rad_np, "ims_correction", lambda *a, **k: 0.0)
     _, utms = disort_rad_forward(prop, bc, nstr=nstr, nmom=nmom, umu=umu, phi=phi, utau=utau,
                                  corint=True)
@@ -334,8 +334,8 @@ def test_radiance_umu0_as_given():
     flux = d.forward(torch.as_tensor(prop, device=DEV), _dev(bc)).cpu().numpy()
     uu = d.get_rad().cpu().numpy()
     fref, uref = disort_rad_forward(prop, bc, None, nstr=nstr, umu=umu, phi=phi, utau=utau)
-    assert _col_err(uu, uref) < TOL, _col_err(uu, uref)
-    assert rel_err(flux, fref).max() < TOL
+    assert margin(_col_err(uu, uref)) < TOL, _col_err(uu, uref)
+    assert margin(rel_err(flux, fref).max()) < TOL
     bc0 = dict(bc, umu0=np.array([[0.5, 0.0, 0.5, 0.5]]))
     with pytest.raises(RuntimeError):
         d.forward(torch.as_tensor(prop, device=DEV), _dev(bc0))
