@@ -19,3 +19,7 @@ for r in $(seq $ROUNDS); do
     done
   done
 done
+# kernel timeline of one C4 step with the team sweep
+HD_SWEEP_TEAM=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/stats_t1 -o kt --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extra > $OUT/stats_t1.json 2> $OUT/stats_t1.err
+python scripts/trace_timeline.py $(ls $OUT/stats_t1/*/kt_kernel_trace.csv | head -1) > $OUT/timeline_t1.txt
+head -30 $OUT/timeline_t1.txt

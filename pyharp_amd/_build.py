@@ -21,13 +21,6 @@ HEADERS = ["hd_device.hpp", "hd_kernels.hpp", "hd_rad.hpp", "hd_team_prims.hpp",
            os.path.join("..", "..", "include", "harp_amd", "ncread.hpp"),
            os.path.join("..", "..", "include", "harp_amd", "nc4read.hpp")]
 ARCH = os.environ.get("HD_OFFLOAD_ARCH", "gfx950")
-# per-source extra flags.  hd_kernels.hip: MachineLICM hoists loop-invariant
-# constants (exp's polynomial, identity-matrix selects, per-element offsets) out of
-# the sweeps' layer loops into live registers; without it the 8-lane team sweep
-# needs 102 VGPRs instead of 122 (it must stay <= 112 to share a SIMD with the
-# 396-register layer kernel) and the one-lane sweep 474
-# instead of 492; the layer kernel is unchanged (no loop around its constants)
-EXTRA = {"hd_kernels.hip": ["-mllvm", "-disable-machine-licm"]}
 
 
 def _hipcc() -> str:
@@ -54,7 +47,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     for src in SOURCES:  # one hipcc per source, in parallel (the team TU dominates)
         obj = os.path.join(CSRC, src + ".o")
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
-               "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj] + EXTRA.get(src, [])
+               "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((cmd, subprocess.Popen(cmd)))

@@ -41,9 +41,6 @@ struct hd_context {
   // team-path Jacobi from the tabulated (ssa, chi_1) eigenvectors
   // (hd_kernels.hpp); HD_JACOBI_WARM=0 in the environment turns it off (A/B)
   int warm = 1;
-  // nstr 16: the adding sweep in 8-lane teams beside the next chunk's layer kernel
-  // (hd_sweep_team_kernel); HD_SWEEP_TEAM=0 in the environment runs the one-lane sweep
-  int team_sweep = 0;
   // true while a solve enqueues into a capturing stream: scratch may not grow then
   bool capturing = false;
   std::string err;
@@ -385,7 +382,6 @@ int hd_context_create(hd_context** out, int device) {
                 ndev);
   hd_context* ctx = new hd_context();
   if (const char* e = std::getenv("HD_JACOBI_WARM")) ctx->warm = std::atoi(e) != 0;
-  if (const char* e = std::getenv("HD_SWEEP_TEAM")) ctx->team_sweep = std::atoi(e) != 0;
   ctx->device = device;
   auto init = [ctx]() -> int {
     HD_HIP(ctx, hipSetDevice(ctx->device));
@@ -722,7 +718,6 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
     sa.cmaj = cmaj;
     sa.nwave = in->nwave;
     sa.beam_scale = beam_in_sweep ? 1 : 0;
-    sa.team_sweep = ctx->team_sweep;
     if (band && reg) {
       sa.wts = band->weight;
       sa.part = part;

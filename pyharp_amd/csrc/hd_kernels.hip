@@ -804,313 +804,6 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
 }
 
 // ============================================================================
-// K2 in 8-lane teams (nstr 16): the adding sweep of hd_sweep_kernel with one
-// solve per team and lane i of the team holding row i of every 8 x 8 matrix
-// (A = Ra, R~, T~, W1, ZT, P) and element i of every vector.  The one-lane sweep
-// needs ~490 registers, so it cannot share a SIMD with the 400-register layer
-// kernel: the two time-share the chip (period = layer alone + sweep alone).  A
-// team lane needs ~100, so this sweep runs on the registers the layer kernel
-// leaves free, beside chunk k+1's layer kernel.  Matrix
-// rows reach the other lanes of a team through LDS (each lane writes its row,
-// the team reads whole rows back: broadcast reads, 8 distinct 16-byte addresses
-// per wave instruction); the pivot-free LU of the one-lane sweep becomes a
-// Gauss-Jordan elimination of [W1 | T~ | v1] (the same pivots), so that lane i
-// ends with row i of ZT = W1^-1 T~ and t1_i = (W1^-1 v1)_i.  The records are the
-// one-lane sweep's (RecL in, RecB out, same elements), so hd_backsub_kernel is
-// unchanged.
-// ============================================================================
-namespace {
-template <int M>
-__device__ __forceinline__ double swz_xor(double x) {  // lane (i ^ M) within 32-lane halves
-  constexpr int pat = 0x1F | (M << 10);
-  const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(x), pat);
-  const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(x), pat);
-  return __hiloint2double(hi, lo);
-}
-// sum over the 8 lanes of a team: a butterfly, so every lane holds the same bits
-__device__ __forceinline__ double team8_sum(double x) {
-  x += swz_xor<1>(x);
-  x += swz_xor<2>(x);
-  x += swz_xor<4>(x);
-  return x;
-}
-__device__ __forceinline__ void lds_order() {
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-}
-}  // namespace
-
-template <int NN>
-__global__ __launch_bounds__(64) void hd_sweep_team_kernel(SweepArgs A) {
-  static_assert(NN == 8, "8-lane teams: one row per lane at nstr 16");
-  constexpr int TS = NN * NN + 2;  // team stride in doubles: the 8 teams' rows on disjoint banks
-  constexpr int PS = 2 * NN + 2;   // pivot row: W1 | T~ | v1 | pad
-  __shared__ __attribute__((aligned(16))) double mat[8 * TS];
-  __shared__ __attribute__((aligned(16))) double piv[8 * PS];
-  constexpr int VS = NN + 2;       // vector stride: disjoint banks too
-  __shared__ __attribute__((aligned(16))) double vec[8 * VS];
-  const Quad<NN>& Qc = quad<NN>();
-  const int lane = (int)threadIdx.x, t = lane >> 3, i = lane & 7;
-  const long sl = (long)blockIdx.x * 8 + t;
-  if (sl >= A.nsc) return;  // a whole team: no lane of it takes part in anything
-  const long s = solve_of(A.s0 + sl, A.cmaj, A.nwave, A.ncol);
-  const int L = A.nlyr;
-  const size_t nsc = A.nsc;
-  using RL = RecL<NN>;
-  using RB = RecB<NN>;
-  int st = 0;
-
-  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
-  const double fb = A.fbeam ? A.fbeam[s] : 0.0;
-  const bool beam = fb > 0.0 && mu0 > 0.0;
-  const double alb = A.albedo ? A.albedo[s] : 0.0;
-  if (!(alb >= 0.0) || !(alb <= 1.0)) st |= kStBadInput;
-  double top = A.fisot ? A.fisot[s] : 0.0;
-  double bsurf = 0.0;
-  if (A.planck) {
-    bsurf = A.planckv[(size_t)(L + 1) * nsc + sl];
-    top += A.planckv[(size_t)(L + 2) * nsc + sl];
-  }
-  const double twopi = 2.0 * kPi;
-  const double rmu0 = beam ? 1.0 / mu0 : 0.0;
-  const double f0mu0 = beam ? fb * mu0 : 0.0;
-  const double g_i = Qc.g[i];
-
-  double* const mt = mat + t * TS;  // this team's matrix rows
-  double* const pv = piv + t * PS;
-  double* const vt = vec + t * VS;
-  // this lane's row of a matrix -> LDS (16-byte stores)
-  auto put_row = [&](const double (&x)[NN]) {
-    double2* p = reinterpret_cast<double2*>(mt + i * NN);
-#pragma unroll
-    for (int q = 0; q < NN / 2; ++q) p[q] = make_double2(x[2 * q], x[2 * q + 1]);
-  };
-  // y += a M for the team matrix M in LDS (row k read whole: broadcast reads),
-  // one row in flight at a time (the scheduler would otherwise issue all 32 reads
-  // up front and hold 128 VGPRs of rows)
-  auto row_times = [&](const double (&a)[NN], double (&y)[NN]) {
-    const double2* p = reinterpret_cast<const double2*>(mt);
-#pragma unroll
-    for (int k = 0; k < NN; ++k) {
-#pragma unroll
-      for (int q = 0; q < NN / 2; ++q) {
-        const double2 v = p[k * (NN / 2) + q];
-        y[2 * q] = fma(a[k], v.x, y[2 * q]);
-        y[2 * q + 1] = fma(a[k], v.y, y[2 * q + 1]);
-      }
-      HD_PHASE();
-    }
-  };
-  // a . x for x distributed over the team (element k from lane k, through LDS)
-  auto dot_team = [&](const double (&a)[NN], double xi, double init) {
-    vt[i] = xi;
-    lds_order();
-    const double2* p = reinterpret_cast<const double2*>(vt);
-    double r = init;
-#pragma unroll
-    for (int q = 0; q < NN / 2; ++q) {
-      const double2 v = p[q];
-      r = fma(a[2 * q], v.x, r);
-      r = fma(a[2 * q + 1], v.y, r);
-    }
-    lds_order();
-    return r;
-  };
-  // record element e of this solve in a layer's record (pair layout [pair][nsc]):
-  // a uniform layer base plus a 32-bit per-lane offset (saddr + voffset loads)
-  // il / sll: this lane's row and solve, laundered once per layer (below) so that the
-  // ~40 per-element offsets are recomputed inside the loop instead of being hoisted
-  // out of it into live registers
-  int il = i;
-  unsigned sll = (unsigned)sl << 4;
-  auto eoff = [&](int e) { return (unsigned)(e >> 1) * (unsigned)nsc * 16u + sll + ((e & 1) << 3); };
-  // fresh copies of il / sll right before a group of accesses: their offsets are
-  // then computed where they are used, not all at the top of the layer
-  auto relaunder = [&]() {
-    il = i;
-    sll = (unsigned)sl << 4;
-    asm volatile("" : "+v"(il), "+v"(sll));
-  };
-  auto ld = [&](const double* base, unsigned off) {
-    return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(base) + off);
-  };
-  auto st8 = [&](double* base, unsigned off, double v) {
-    *reinterpret_cast<double*>(reinterpret_cast<char*>(base) + off) = v;
-  };
-  // row i of a symmetric record matrix (packed upper triangle at element e0)
-  auto load_row = [&](const double* base, int e0, double (&x)[NN]) {
-    relaunder();
-#pragma unroll
-    for (int j = 0; j < NN; ++j) x[j] = ld(base, eoff(e0 + sym_index<NN>(il, j)));
-  };
-
-  double ra[NN];  // row i of the reflection of the stack above
-#pragma unroll
-  for (int j = 0; j < NN; ++j) ra[j] = 0.0;
-  double sd = g_i * top;  // diffuse downward source at the current interface
-  double tauc = 0.0;
-
-  for (int lc = 0; lc < L; ++lc) {
-    const double* lb = A.scr + (size_t)lc * RL::pairs * nsc * 2;  // uniform
-    double* bb = A.bsub + (size_t)lc * RB::pairs * nsc * 2;
-    il = i;
-    sll = (unsigned)sl << 4;
-    asm volatile("" : "+v"(il), "+v"(sll));
-    const double eb = exp(-tauc * rmu0);
-    const double sscale = A.beam_scale ? eb : 1.0;
-    const double spl = ld(lb, eoff(RL::Sp + il)) * sscale;
-    const double taup = ld(lb, eoff(RL::Tau));
-
-    // level lc (top of layer lc): F_dn = rc . I+ + cs  (A symmetric: column i = row i)
-    {
-      double rc = 0.0;
-#pragma unroll
-      for (int j = 0; j < NN; ++j) rc = fma(ra[j], Qc.g[j], rc);
-      st8(bb, eoff(RB::Rc + il), twopi * rc);
-      const double cs = team8_sum(g_i * sd);
-      if (i == 0) st8(bb, eoff(RB::Cs), fma(twopi, cs, f0mu0 * eb));
-    }
-    // W1 = I - R A (row i), v1 = R Sd + S+.  A's rows stay in LDS until P = A ZT
-    // below: ra is not live across the elimination
-    double w[NN], v;
-    put_row(ra);
-    lds_order();
-    {
-      double r[NN];
-      load_row(lb, RL::R, r);
-#pragma unroll
-      for (int j = 0; j < NN; ++j) w[j] = 0.0;
-      row_times(r, w);
-      lds_order();
-#pragma unroll
-      for (int j = 0; j < NN; ++j) w[j] = (i == j ? 1.0 : 0.0) - w[j];
-      v = dot_team(r, sd, spl);
-    }
-    HD_PHASE();
-    // Gauss-Jordan on [W1 | T~ | v1], no pivoting (the LU pivots of the one-lane
-    // sweep), rows not normalised until the end: lane i ends with d_i [e_i | ZT_i | t1_i]
-    double z[NN], d = 1.0;
-    load_row(lb, RL::T, z);
-#pragma unroll
-    for (int k = 0; k < NN; ++k) {
-      if (i == k) {
-        double2* p = reinterpret_cast<double2*>(pv);
-#pragma unroll
-        for (int q = k / 2; q < NN / 2; ++q) p[q] = make_double2(w[2 * q], w[2 * q + 1]);
-#pragma unroll
-        for (int q = 0; q < NN / 2; ++q) p[NN / 2 + q] = make_double2(z[2 * q], z[2 * q + 1]);
-        p[NN] = make_double2(v, 0.0);
-      }
-      lds_order();
-      const double2* p = reinterpret_cast<const double2*>(pv);
-      const double2 pkk = p[k / 2];
-      const double pk = (k & 1) ? pkk.y : pkk.x;
-      // the pivot test and d are pinned at this step: left free, the compiler sinks
-      // them past the loop and keeps all NN pivots live
-      st |= fabs(pk) > 1.0e-12 ? 0 : kStPivot;
-      d = i == k ? pk : d;
-      asm volatile("" : "+v"(st), "+v"(d));
-      const double f = i == k ? 0.0 : w[k] * rcp_nr(pk);
-      if (k & 1) {
-      } else if (k + 1 < NN) {
-        w[k + 1] = fma(-f, pkk.y, w[k + 1]);
-      }
-#pragma unroll
-      for (int q = k / 2 + 1; q < NN / 2; ++q) {
-        const double2 x = p[q];
-        w[2 * q] = fma(-f, x.x, w[2 * q]);
-        w[2 * q + 1] = fma(-f, x.y, w[2 * q + 1]);
-      }
-      HD_PHASE();
-#pragma unroll
-      for (int q = 0; q < NN / 2; ++q) {
-        const double2 x = p[NN / 2 + q];
-        z[2 * q] = fma(-f, x.x, z[2 * q]);
-        z[2 * q + 1] = fma(-f, x.y, z[2 * q + 1]);
-      }
-      v = fma(-f, p[NN].x, v);
-      lds_order();
-    }
-    {
-      const double rd = rcp_nr(d);
-#pragma unroll
-      for (int j = 0; j < NN; ++j) z[j] *= rd;  // row i of ZT
-      v *= rd;                                  // t1_i
-    }
-    // ZT column-major (element j NN + i), t1
-    relaunder();
-#pragma unroll
-    for (int j = 0; j < NN; ++j) st8(bb, eoff(RB::Z + j * NN + il), z[j]);
-    st8(bb, eoff(RB::Tv + il), v);
-    HD_PHASE();
-    // A's row i back from LDS; u = A t1 + Sd ; P = A ZT (into w)
-    {
-      const double2* p = reinterpret_cast<const double2*>(mt + i * NN);
-#pragma unroll
-      for (int q = 0; q < NN / 2; ++q) {
-        const double2 x = p[q];
-        ra[2 * q] = x.x;
-        ra[2 * q + 1] = x.y;
-      }
-    }
-    lds_order();
-    const double u = dot_team(ra, v, sd);
-#pragma unroll
-    for (int j = 0; j < NN; ++j) w[j] = 0.0;
-    put_row(z);
-    lds_order();
-    row_times(ra, w);
-    lds_order();
-    HD_PHASE();
-    // Ra <- R + T P ; Sd <- T u + S-   (R~, T~ rows read again: L2 hits)
-    put_row(w);
-    lds_order();
-    {
-      double tr[NN];
-      load_row(lb, RL::T, tr);
-      load_row(lb, RL::R, ra);
-      row_times(tr, ra);
-      lds_order();
-      relaunder();
-      sd = dot_team(tr, u, ld(lb, eoff(RL::Sm + il)) * sscale);
-    }
-    tauc += taup;
-  }
-
-  // ---- Lambertian surface: I+ = g x ----
-  double rgi = 0.0;  // (Ra g)_i
-#pragma unroll
-  for (int j = 0; j < NN; ++j) rgi = fma(ra[j], Qc.g[j], rgi);
-  const double gsd = team8_sum(g_i * sd);
-  const double grg = team8_sum(g_i * rgi);
-  double esurf = (1.0 - alb) * bsurf;
-  const double dirsurf = f0mu0 * exp(-tauc * rmu0);
-  if (beam) esurf += alb * dirsurf / kPi;
-  const double x = (2.0 * alb * gsd + esurf) / (1.0 - 2.0 * alb * grg);
-  // up = sum g_i (g_i x), dn = sum g_i (Sd_i + (Ra g x)_i)
-  const double up = team8_sum(g_i * (g_i * x));
-  const double dn = team8_sum(g_i * fma(rgi, x, sd));
-  const double f0 = twopi * up, f1 = twopi * dn + dirsurf;
-  if (i == 0) {
-    if (A.flux) {
-      double* fo = A.flux + (size_t)s * (L + 1) * 2;
-      fo[0] = f0;
-      fo[1] = f1;
-    }
-    if (A.fsurf) {
-      A.fsurf[sl] = f0;
-      A.fsurf[nsc + sl] = f1;
-    }
-    A.xsurf[sl] = x;
-  }
-  if (!isfinite(f0 + f1)) st |= kStNonFinite;
-  if (st && i == 0) {
-    atomicOr(&A.status[s], st);
-    if (st & 0x0F) atomicOr(A.anyerr, 1);
-  }
-}
-
-// ============================================================================
 // K3: per-solve back-substitution bottom -> top.  Split from the adding sweep
 // so that it runs at the occupancy of its own small register footprint (the
 // sweep's register file allows one wave per SIMD): a pure stream over the
@@ -1457,19 +1150,6 @@ void launch_prologue(const PlanckArgs* pa, const TaucArgs* ta, hipStream_t strea
 }
 
 template <int NN>
-static void launch_sweep(const SweepArgs& sa, hipStream_t stream) {
-  if constexpr (NN == 8) {
-    if (sa.team_sweep) {  // 8-lane teams, one solve per team
-      hipLaunchKernelGGL(hd_sweep_team_kernel<NN>, dim3((unsigned)((sa.nsc + 7) / 8)), dim3(64), 0,
-                         stream, sa);
-      return;
-    }
-  }
-  hipLaunchKernelGGL(hd_sweep_kernel<NN>, dim3((unsigned)((sa.nsc + 63) / 64)), dim3(64), 0,
-                     stream, sa);
-}
-
-template <int NN>
 static hipError_t launch_chunk(const PlanckArgs* pa, const TaucArgs* ta, const LayerArgs& la,
                                const SweepArgs& sa, hipStream_t stream, hipEvent_t* ev) {
   launch_prologue(pa, ta, stream);
@@ -1479,9 +1159,8 @@ static hipError_t launch_chunk(const PlanckArgs* pa, const TaucArgs* ta, const L
   if (ev) (void)hipEventRecord(ev[0], stream);
   hipLaunchKernelGGL(hd_layer_kernel<NN>, dim3(nb1), dim3(kLayerBlock), 0, stream, la);
   if (ev) (void)hipEventRecord(ev[1], stream);
-  launch_sweep<NN>(sa, stream);
+  hipLaunchKernelGGL(hd_sweep_kernel<NN>, dim3(nb2), dim3(64), 0, stream, sa);
   if (ev) (void)hipEventRecord(ev[2], stream);
-  (void)nb2;
   return hipGetLastError();
 }
 
@@ -1532,7 +1211,11 @@ static void launch_layer(const LayerArgs& la, hipStream_t stream) {
                                   ((la.nlyr + kLayersPerBlock - 1) / kLayersPerBlock));
   hipLaunchKernelGGL(hd_layer_kernel<NN>, dim3(nb1), dim3(kLayerBlock), 0, stream, la);
 }
-
+template <int NN>
+static void launch_sweep(const SweepArgs& sa, hipStream_t stream) {
+  hipLaunchKernelGGL(hd_sweep_kernel<NN>, dim3((unsigned)((sa.nsc + 63) / 64)), dim3(64), 0,
+                     stream, sa);
+}
 hipError_t launch_layer_nn(int nn, const LayerArgs& la, hipStream_t stream) {
   switch (nn) {
     case 1: launch_layer<1>(la, stream); break;

@@ -165,8 +165,6 @@ struct SweepArgs {
   // register path: the layer records' sources are for a unit beam at each layer
   // top (LayerArgs.tauc null); the sweep scales them by exp(-tau_c/mu0)
   int beam_scale;
-  // register path, nstr 16: the adding sweep in 8-lane teams (hd_sweep_team_kernel)
-  int team_sweep;
 };
 
 // chunk epilogue of the fused band sum: bflux[c] (=|+=) sum of the chunk's
