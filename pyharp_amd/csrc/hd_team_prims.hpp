@@ -146,8 +146,8 @@ __device__ __forceinline__ bool team_chol(double (&a)[NN], double (&lt)[NN], dou
     d = d > 1.0e-300 ? d : 1.0e-300;
     const double r = rsq_nr(d);
     const double lkk = d * r;
-    const double aik = a[k] * r;
-    a[k] = i > k ? aik : (i == k ? lkk : 0.0);
+    const double aik = a[k] * r;  // on lane k: d r = lkk (d is lane k's a[k])
+    a[k] = i >= k ? aik : 0.0;
     if (i == k) rd = r;
     if constexpr (WANT_LT) {
       if (i == k) lt[k] = lkk;
@@ -260,14 +260,21 @@ __device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double& own, 
 #else
   const double gam = g0 + g1;
 #endif
-  const bool lo = i < pi;
-  const double app = lo ? own : oth;
-  const double aqq = lo ? oth : own;
+  // the lane with the lower index (bit hb of i clear) holds column p, its partner q;
+  // the q side's sign flips are XORs of the sign bit (no 64-bit selects):
+  // d = a_qq - a_pp, se = -s on the p side, the norm update's cross term
+  constexpr int hb = M >= 8 ? 3 : M >= 4 ? 2 : M >= 2 ? 1 : 0;
+  const int qside = (i >> hb) & 1;
+  const int qmask = (int)((unsigned)qside << 31);  // sign flip on the q side
+  const int pmask = (int)((unsigned)qmask ^ 0x80000000u);  // sign flip on the p side
+  auto flip = [](double x, int m) {
+    return __hiloint2double(__double2hiint(x) ^ m, __double2loint(x));
+  };
   const bool pair = i < NN && pi < NN;
-  const double g2 = gam * gam, pq = app * aqq;
+  const double g2 = gam * gam, pq = own * oth;
   const bool r = on && pair && g2 > kJacobiTol2 * pq;
   off += pair ? g2 : 0.0;  // each pair counted by both of its lanes
-  const double d = aqq - app;
+  const double d = flip(oth - own, qmask);  // a_qq - a_pp on both sides (bitwise equal)
 #if HD_JACOBI_F32_ANGLE
   // the angle in FP32, c and s normalised in FP64 (see jacobi_os_round)
   const float df = (float)d, g2f = 2.0f * (float)gam;
@@ -286,7 +293,7 @@ __device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double& own, 
   const double c = r ? u * z : 1.0;
   const double s = r ? sg * gam * z : 0.0;
 #endif
-  const double se = lo ? -s : s;  // p side: c b_p - s b_q ; q side: s b_p + c b_q
+  const double se = flip(s, pmask);  // p side: c b_p - s b_q ; q side: s b_p + c b_q
 #if HD_JACOBI_SCALED
   const double tq = se * sq * rcp_nr(c * sig);
   sfor<0, NN>([&](auto K) { b[HD_K(K)] = fma(tq, bq[HD_K(K)], b[HD_K(K)]); });
@@ -295,9 +302,9 @@ __device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double& own, 
   (void)sig;
   sfor<0, NN>([&](auto K) { b[HD_K(K)] = fma(se, bq[HD_K(K)], c * b[HD_K(K)]); });
 #endif
-  // rotated norms: |c b_p - s b_q|^2 and |s b_p + c b_q|^2
+  // rotated norms: |c b_p - s b_q|^2 and |s b_p + c b_q|^2 (own: this lane's column)
   const double cc = c * c, ss2 = s * s, cs2 = 2.0 * c * s * gam;
-  own = lo ? fma(cc, app, fma(ss2, aqq, -cs2)) : fma(ss2, app, fma(cc, aqq, cs2));
+  own = fma(cc, own, fma(ss2, oth, flip(cs2, pmask)));
 }
 
 // Sweeps of rounds 1..15 until the sweep that was the last one needed
