@@ -72,6 +72,7 @@ struct hd_context {
   size_t hstage_len = 0;  // doubles
   hipStream_t hstream = nullptr;   // host<->device copies
   hipStream_t hstream2 = nullptr;  // the pieces' solves
+  hipStream_t hstream3 = nullptr;  // device->host copies (PCIe is full duplex: beside the uploads)
   hipEvent_t hev_in[2] = {nullptr, nullptr};
   hipEvent_t hev_done[2] = {nullptr, nullptr};
 };
@@ -422,6 +423,7 @@ int hd_context_destroy(hd_context* ctx) {
   if (ctx->hstage) (void)hipFree(ctx->hstage);
   if (ctx->hstream) (void)hipStreamDestroy(ctx->hstream);
   if (ctx->hstream2) (void)hipStreamDestroy(ctx->hstream2);
+  if (ctx->hstream3) (void)hipStreamDestroy(ctx->hstream3);
   for (int b = 0; b < 2; ++b) {
     if (ctx->hev_in[b]) (void)hipEventDestroy(ctx->hev_in[b]);
     if (ctx->hev_done[b]) (void)hipEventDestroy(ctx->hev_done[b]);
@@ -935,6 +937,7 @@ int solve_host(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, doubl
   HD_HIP(ctx, hipSetDevice(ctx->device));
   if (!ctx->hstream) HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->hstream, hipStreamNonBlocking));
   if (!ctx->hstream2) HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->hstream2, hipStreamNonBlocking));
+  if (!ctx->hstream3) HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->hstream3, hipStreamNonBlocking));
   for (int b = 0; b < 2; ++b) {
     if (!ctx->hev_in[b]) HD_HIP(ctx, hipEventCreateWithFlags(&ctx->hev_in[b], hipEventDisableTiming));
     if (!ctx->hev_done[b])
@@ -952,16 +955,19 @@ int solve_host(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, doubl
     }
     ctx->hstage_len = total;
   }
-  hipStream_t cs = ctx->hstream, xs = ctx->hstream2;  // copies, solves
+  // uploads, solves, downloads: the per-point fluxes of piece j go back on their own
+  // stream while piece j+2's arrays go up (both PCIe directions at once)
+  hipStream_t cs = ctx->hstream, xs = ctx->hstream2, ds = ctx->hstream3;
   // whatever happens below, nothing may still be reading or writing the
   // caller's arrays when this returns
   struct Drain {
-    hipStream_t a, b;
+    hipStream_t a, b, c;
     ~Drain() {
       (void)hipStreamSynchronize(a);
       (void)hipStreamSynchronize(b);
+      (void)hipStreamSynchronize(c);
     }
-  } drain_on_exit{cs, xs};
+  } drain_on_exit{cs, xs, ds};
   double* q = ctx->hstage;
   double* inbuf[2] = {q, q + pin};
   q += 2 * pin;
@@ -997,11 +1003,11 @@ int solve_host(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, doubl
   auto d2h = [&](int j) -> int {  // piece j's per-point fluxes and status, after its solve
     const long w0 = (long)j * wpp, wj = std::min<long>(wpp, in->nwave - w0);
     const size_t o = (size_t)w0 * ncol, n = (size_t)wj * ncol;
-    HD_HIP(ctx, hipStreamWaitEvent(cs, ctx->hev_done[j & 1], 0));
+    HD_HIP(ctx, hipStreamWaitEvent(ds, ctx->hev_done[j & 1], 0));
     if (flux)
       HD_HIP(ctx, hipMemcpyAsync(flux + o * nlev2, flux_d + o * nlev2, n * nlev2 * sizeof(double),
-                                 hipMemcpyDeviceToHost, cs));
-    HD_HIP(ctx, hipMemcpyAsync(st_out + o, st_d + o, n * sizeof(int), hipMemcpyDeviceToHost, cs));
+                                 hipMemcpyDeviceToHost, ds));
+    HD_HIP(ctx, hipMemcpyAsync(st_out + o, st_d + o, n * sizeof(int), hipMemcpyDeviceToHost, ds));
     return HD_OK;
   };
   for (int j = 0; j < npiece; ++j) {
@@ -1047,11 +1053,12 @@ int solve_host(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, doubl
     rc = hd_band_flux(part_d, w_d + in->nwave, npiece, (int)ncol, nlev, bsum, xs);
     if (rc) return fail(ctx, rc, "%s: band sum: %s", what, hd_last_error(nullptr));
     HD_HIP(ctx, hipEventRecord(ctx->hev_done[0], xs));
-    HD_HIP(ctx, hipStreamWaitEvent(cs, ctx->hev_done[0], 0));
-    HD_HIP(ctx, hipMemcpyAsync(bflux, bsum, ncol * nlev2 * sizeof(double), hipMemcpyDeviceToHost, cs));
+    HD_HIP(ctx, hipStreamWaitEvent(ds, ctx->hev_done[0], 0));
+    HD_HIP(ctx, hipMemcpyAsync(bflux, bsum, ncol * nlev2 * sizeof(double), hipMemcpyDeviceToHost, ds));
   }
   HD_HIP(ctx, hipStreamSynchronize(cs));
   HD_HIP(ctx, hipStreamSynchronize(xs));
+  HD_HIP(ctx, hipStreamSynchronize(ds));
   for (size_t i = 0; i < ns; ++i)
     if (st_out[i] & HD_STATUS_ERROR_MASK)
       return fail(ctx, HD_ENUMERIC,
