@@ -41,6 +41,9 @@ struct hd_context {
   // team-path Jacobi from the tabulated (ssa, chi_1) eigenvectors
   // (hd_kernels.hpp); HD_JACOBI_WARM=0 in the environment turns it off (A/B)
   int warm = 1;
+  // team path: the two-waves-per-SIMD sweep (hd_team_mfma_sweep_lean_kernel);
+  // HD_TEAM_SWEEP_LEAN=0/1 in the environment picks it when a context is created
+  int lean = 0;
   // true while a solve enqueues into a capturing stream: scratch may not grow then
   bool capturing = false;
   std::string err;
@@ -383,6 +386,7 @@ int hd_context_create(hd_context** out, int device) {
                 ndev);
   hd_context* ctx = new hd_context();
   if (const char* e = std::getenv("HD_JACOBI_WARM")) ctx->warm = std::atoi(e) != 0;
+  if (const char* e = std::getenv("HD_TEAM_SWEEP_LEAN")) ctx->lean = std::atoi(e) != 0;
   ctx->device = device;
   auto init = [ctx]() -> int {
     HD_HIP(ctx, hipSetDevice(ctx->device));
@@ -720,6 +724,7 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
     sa.cmaj = cmaj;
     sa.nwave = in->nwave;
     sa.beam_scale = beam_in_sweep ? 1 : 0;
+    sa.lean = ctx->lean;
     if (band && reg) {
       sa.wts = band->weight;
       sa.part = part;

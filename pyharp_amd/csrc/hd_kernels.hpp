@@ -165,6 +165,9 @@ struct SweepArgs {
   // register path: the layer records' sources are for a unit beam at each layer
   // top (LayerArgs.tauc null); the sweep scales them by exp(-tau_c/mu0)
   int beam_scale;
+  // team path (nstr 18..32): the lean sweep (hd_team_mfma_sweep_lean_kernel, two waves
+  // per SIMD) instead of the one-wave-per-SIMD sweep
+  int lean;
 };
 
 // chunk epilogue of the fused band sum: bflux[c] (=|+=) sum of the chunk's

@@ -832,6 +832,304 @@ __global__ __launch_bounds__(64, 1) void hd_team_mfma_sweep_kernel(SweepArgs A) 
 
 
 // ============================================================================
+// K2 (team, MFMA), lean: the same sweep and back-substitution as
+// hd_team_mfma_sweep_kernel in at most 256 registers, so that two waves share a
+// SIMD (and one can run beside a 240-register layer-kernel wave) instead of one.
+// What changes is only where the operands live between their uses:
+//   * A's team rows (for the level's rc, and u = A t1 + Sd) stay in LDS tile set
+//     S0 from the end of one layer to the middle of the next, not in registers;
+//     W1 = I - R A goes through tile set S1 instead;
+//   * R~ and T~ are read from the layer record where they are needed -- R~ (M
+//     layout) for W1 and again for A <- R~ + T~ (A ZT), R~'s team row for v1, T~'s
+//     team row for Sd, T~ (M layout) for the ZT products -- instead of all at the
+//     top of the layer (second reads of a record are L2 hits);
+//   * per-element record offsets are recomputed where they are used (laundered
+//     lane indices), not hoisted out of the layer loop.
+// The arithmetic and its order are hd_team_mfma_sweep_kernel's, so the records
+// and fluxes are bitwise the same (tests/test_gpu_parity.py: lean vs default).
+// ============================================================================
+template <int NN>
+__global__ __launch_bounds__(64, 2) void hd_team_mfma_sweep_lean_kernel(SweepArgs A) {
+  __shared__ double lds[2 * kSet];
+  double* S0 = lds;
+  double* S1 = lds + kSet;
+  const Quad<NN>& Qc = tquad<NN>(c_qt);
+  const int lane = (int)threadIdx.x;
+  const int h = lane >> 4, c = lane & 15;  // M layout
+  const int t = h, i = c;                  // T layout: team t, row i
+  const bool act = i < NN;
+  const int ii = act ? i : 0;
+  const int grp = (int)blockIdx.x;
+  const bool valid = grp * 4 + t < A.nsc;
+  const int sl = valid ? grp * 4 + t : grp * 4;
+  const long s = solve_of(A.s0 + sl, A.cmaj, A.nwave, A.ncol);
+  const int L = A.nlyr;
+  const size_t nsc = A.nsc;
+  int st = 0;
+  const double msk = act ? 1.0 : 0.0;
+  const double g_i = Qc.g[ii] * msk;
+
+  for (int k = lane; k < 2 * kSet; k += 64) lds[k] = 0.0;  // A = 0 in S0
+  lds_fence();
+
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
+  const double fb = A.fbeam ? A.fbeam[s] : 0.0;
+  const bool beam = fb > 0.0 && mu0 > 0.0;
+  const double alb = A.albedo ? A.albedo[s] : 0.0;
+  if (!(alb >= 0.0) || !(alb <= 1.0)) st |= kStBadInput;
+  double top = A.fisot ? A.fisot[s] : 0.0;
+  double bsurf = 0.0;
+  if (A.planck) {
+    bsurf = A.planckv[(size_t)(L + 1) * nsc + sl];
+    top += A.planckv[(size_t)(L + 2) * nsc + sl];
+  }
+  const double twopi = 2.0 * kPi;
+  const double rmu0 = beam ? 1.0 / mu0 : 0.0;
+  const double f0mu0 = beam ? fb * mu0 : 0.0;
+  const int g0 = grp * 4;  // the wave's first solve (uniform)
+
+  // problem tt's record element (r, c) of the matrix at offset off, M layout
+  auto load_m = [&](int lc, int off, double (&x)[4][4]) {
+    __builtin_amdgcn_sched_barrier(0);  // issued here, not hoisted into an earlier phase
+    int hl = h, cl = c;
+    asm volatile("" : "+v"(hl), "+v"(cl));
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      const int slt = g0 + tt < A.nsc ? g0 + tt : g0;
+      const double* rt = A.scr + ((size_t)lc * nsc + slt) * ne1t<NN>() + off;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int r = hl + 4 * m;
+        const bool in = r < NN && cl < NN;
+        x[tt][m] = in ? rt[in ? r * NN + cl : 0] : 0.0;
+      }
+    }
+  };
+  // this problem's team row of the matrix at offset off
+  auto load_row = [&](const double* rec, int off, double (&x)[NN]) {
+    __builtin_amdgcn_sched_barrier(0);
+    int il = ii;
+    asm volatile("" : "+v"(il));
+    sfor<0, NN>([&](auto J) { x[HD_K(J)] = rec[off + il * NN + HD_K(J)] * msk; });
+  };
+
+  double ram[4][4];  // A (M layout)
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) ram[tt][m] = 0.0;
+  double sd = g_i * top;
+  double tauc = 0.0;
+
+  for (int lc = 0; lc < L; ++lc) {
+    // the lane indices, laundered per layer: every lane-dependent constant below
+    // (identity entries, triangle masks) is then formed where it is used instead
+    // of all being hoisted out of the loop into live (and spilled) registers
+    int i_ = i, h_ = h, c_ = c;
+    asm volatile("" : "+v"(i_), "+v"(h_), "+v"(c_));
+    const int i = i_, h = h_, c = c_;
+    const double* rec = A.scr + ((size_t)lc * nsc + sl) * ne1t<NN>();
+    double* bp = A.bsub + ((size_t)lc * nsc + sl) * ne2t<NN>();
+    double* bw = (act && valid) ? bp : A.sink;
+    const double spl = rec[2 * NN * NN + ii] * msk;
+
+    // level lc (top of layer lc): F_dn = rc . I+ + cs; A's row i from S0
+    {
+      double ar[NN];
+      get_rows<NN>(S0, t, i, ar);
+      double tq = 0.0;
+      sfor<0, NN>([&](auto J) { tq = fma(ar[HD_K(J)] * msk, Qc.g[HD_K(J)], tq); });
+      bw[NN * NN + NN + ii] = twopi * tq;
+      const double cs = team_sum(g_i * sd);
+      if (i == 0 && valid) bp[NN * NN + 2 * NN] = fma(twopi, cs, f0mu0 * exp(-tauc * rmu0));
+    }
+    // W1 = I - R A on the matrix core, to team rows through S1
+    double w[NN];
+    {
+      double rm[4][4], pw[4][4];
+      load_m(lc, 0, rm);
+      mprod<false>(rm, ram, pw, h, c);
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) pw[tt][m] = (h + 4 * m == c ? 1.0 : 0.0) - pw[tt][m];
+      lds_fence();
+      put_m(S1, h, c, pw);
+      lds_fence();
+    }
+    get_rows<NN>(S1, t, i, w);
+    sfor<0, NN>([&](auto J) { w[HD_K(J)] *= msk; });
+    // t1 = R Sd + S+ (R's team row read here)
+    double t1 = spl;
+    {
+      double rl[NN];
+      load_row(rec, 0, rl);
+      sfor<0, NN>([&](auto K) { t1 = fma(rl[HD_K(K)], bc<HD_K(K)>(sd), t1); });
+    }
+    // LU without pivoting; reciprocal pivots on the diagonal
+    sfor<0, NN>([&](auto K) {
+      constexpr int k = HD_K(K);
+      const double piv = bc<k>(w[k]);
+      if (!(fabs(piv) > 1.0e-12)) st |= kStPivot;
+      const double rp = rcp_nr(piv);
+      const double lik = w[k] * rp;
+      const double mm = i > k ? lik : 0.0;
+      w[k] = i == k ? rp : (i > k ? lik : w[k]);
+      sfor<k + 1, NN>([&](auto J) {
+        constexpr int j = HD_K(J);
+        w[j] = fma(-mm, bc<k>(w[j]), w[j]);
+      });
+      pin<NN>(w);  // this step's broadcasts stay in this step
+    });
+    // t1 <- W1^-1 t1
+    sfor<0, NN>([&](auto K) {
+      constexpr int k = HD_K(K);
+      const double tk = bc<k>(t1);
+      if (i > k) t1 = fma(-w[k], tk, t1);
+    });
+    sfor_rev<0, NN>([&](auto K) {
+      constexpr int k = HD_K(K);
+      if (i == k) t1 *= w[k];
+      const double tk = bc<k>(t1);
+      if (i < k) t1 = fma(-w[k], tk, t1);
+    });
+    // u = A t1 + Sd (A's row i from S0)
+    double u = sd;
+    {
+      double ar[NN];
+      get_rows<NN>(S0, t, i, ar);
+      sfor<0, NN>([&](auto K) { u = fma(ar[HD_K(K)] * msk, bc<HD_K(K)>(t1), u); });
+    }
+    bw[NN * NN + ii] = t1;
+    // columns of L^-1 and U^-1 from the LU rows (hd_team_mfma_sweep_kernel)
+    {
+      double zl[NN], zu[NN];
+      sfor<0, NN>([&](auto R) {
+        constexpr int r = HD_K(R);
+        double v = i == r ? 1.0 : 0.0;
+        sfor<0, r>([&](auto K) { v = fma(-bc<r>(w[HD_K(K)]), zl[HD_K(K)], v); });
+        zl[r] = v;
+        pin<NN>(w);
+      });
+      sfor_rev<0, NN>([&](auto R) {
+        constexpr int r = HD_K(R);
+        double v = i == r ? 1.0 : 0.0;
+        sfor<r + 1, NN>([&](auto K) { v = fma(-bc<r>(w[HD_K(K)]), zu[HD_K(K)], v); });
+        zu[r] = v * bc<r>(w[r]);
+        pin<NN>(w);
+      });
+      sfor<0, NN>([&](auto J) {
+        zl[HD_K(J)] *= msk;
+        zu[HD_K(J)] *= msk;
+      });
+      lds_fence();
+      put_rows<NN>(S0, t, i, zl);  // L^-T, row-major (A's rows in S0 are done)
+      put_rows<NN>(S1, t, i, zu);  // U^-T, row-major
+    }
+    // Sd <- T u + S- (T's team row read here)
+    {
+      double tr[NN];
+      load_row(rec, NN * NN, tr);
+      double tq = rec[2 * NN * NN + NN + ii] * msk;
+      sfor<0, NN>([&](auto K) { tq = fma(tr[HD_K(K)], bc<HD_K(K)>(u), tq); });
+      sd = tq * msk;
+    }
+    lds_fence();
+    // ZT = U^-1 (L^-1 T); record; A <- R + T (A ZT); A's rows to S0 for the next layer
+    {
+      double li[4][4], x1[4][4], zm[4][4];
+      {
+        double tm[4][4];
+        load_m(lc, NN * NN, tm);
+        get_m(S0, h, c, li);
+        mprod<false>(li, tm, x1, h, c);  // L^-1 T
+      }
+      get_m(S1, h, c, li);
+      mprod<false>(li, x1, zm, h, c);  // ZT = U^-1 (L^-1 T)
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        double* zr = A.bsub + ((size_t)lc * nsc + (g0 + tt < A.nsc ? g0 + tt : g0)) * ne2t<NN>();
+        const bool ok = g0 + tt < A.nsc;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int r = h + 4 * m;
+          if (ok && r < NN && c < NN) zr[r * NN + c] = zm[tt][m];
+        }
+      }
+      double pm[4][4];
+      mprod<false>(ram, zm, pm, h, c);  // A ZT   (A symmetric: its own transpose)
+      {
+        double tm[4][4];
+        load_m(lc, NN * NN, tm);
+        mprod<false>(tm, pm, ram, h, c);  // T (A ZT)
+      }
+      {
+        double rm[4][4];
+        load_m(lc, 0, rm);
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+          for (int m = 0; m < 4; ++m) ram[tt][m] += rm[tt][m];
+      }
+      lds_fence();
+      put_m(S0, h, c, ram);
+      lds_fence();
+    }
+    tauc += rec[2 * NN * NN + 2 * NN];
+  }
+
+  // ---- Lambertian surface: I+ = g x ----
+  double rgrow = 0.0;
+  {
+    double ar[NN];
+    get_rows<NN>(S0, t, i, ar);
+    sfor<0, NN>([&](auto J) { rgrow = fma(ar[HD_K(J)] * msk, Qc.g[HD_K(J)], rgrow); });
+  }
+  const double gsd = bc<0>(team_sum(g_i * sd));
+  const double grg = bc<0>(team_sum(g_i * rgrow));
+  double esurf = (1.0 - alb) * bsurf;
+  const double dirsurf = f0mu0 * exp(-tauc * rmu0);
+  if (beam) esurf += alb * dirsurf / kPi;
+  const double x = (2.0 * alb * gsd + esurf) / (1.0 - 2.0 * alb * grg);
+  double ip = g_i * x;
+  double* fo = A.flux + (size_t)(A.flux_local ? (long)sl : s) * (L + 1) * 2;
+  double chk = 0.0;
+  {
+    const double up = team_sum(g_i * ip);
+    const double dn = team_sum(g_i * fma(rgrow, x, sd));
+    if (i == 0 && valid) {
+      fo[0] = twopi * up;
+      fo[1] = twopi * dn + dirsurf;
+    }
+    chk += twopi * up + twopi * dn;
+  }
+  // ---- back-substitution bottom -> top ----
+  for (int lc = L - 1; lc >= 0; --lc) {
+    const double* bp = A.bsub + ((size_t)lc * nsc + sl) * ne2t<NN>();
+    double nip = bp[NN * NN + ii] * msk;
+    sfor<0, NN>([&](auto J) {
+      const double z = bp[ii * NN + HD_K(J)] * msk;
+      nip = fma(z, bc<HD_K(J)>(ip), nip);
+    });
+    const double rc = bp[NN * NN + NN + ii] * msk;
+    const double up = team_sum(g_i * nip);
+    const double dn = team_sum(rc * nip);
+    ip = nip;
+    if (i == 0 && valid) {
+      const int lev = L - lc;
+      fo[2 * lev] = twopi * up;
+      fo[2 * lev + 1] = bp[NN * NN + 2 * NN] + dn;
+    }
+    chk += twopi * up + dn;
+  }
+  if (!isfinite(chk)) st |= kStNonFinite;
+  if (valid && st) {
+    atomicOr(&A.status[s], st);
+    if (st & 0x0F) atomicOr(A.anyerr, 1);
+  }
+}
+
+// ============================================================================
 // Intensity path, nstr 18..32: hd_rad.hip's per-(unit, layer) setup
 // (hd_rad_layer_kernel: the flux layer setup for azimuthal mode m with the
 // Y_l^m(mu_i) tables, parity of l+m, beam source x (2 - delta_m0), thermal only
@@ -1510,8 +1808,12 @@ static hipError_t launch_layer(const LayerArgs& la, hipStream_t stream) {
 
 template <int NN>
 static hipError_t launch_sweep(const SweepArgs& sa, hipStream_t stream) {
-  hipLaunchKernelGGL(hd_team_mfma_sweep_kernel<NN>, dim3((unsigned)((sa.nsc + 3) / 4)), dim3(64),
-                     0, stream, sa);
+  if (sa.lean)
+    hipLaunchKernelGGL(hd_team_mfma_sweep_lean_kernel<NN>, dim3((unsigned)((sa.nsc + 3) / 4)),
+                       dim3(64), 0, stream, sa);
+  else
+    hipLaunchKernelGGL(hd_team_mfma_sweep_kernel<NN>, dim3((unsigned)((sa.nsc + 3) / 4)), dim3(64),
+                       0, stream, sa);
   return hipGetLastError();
 }
 
