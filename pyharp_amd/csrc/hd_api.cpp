@@ -44,6 +44,8 @@ struct hd_context {
   // team path: the two-waves-per-SIMD sweep (hd_team_mfma_sweep_lean_kernel);
   // HD_TEAM_SWEEP_LEAN=0/1 in the environment picks it when a context is created
   int lean = 0;
+  // nstr 4 / 8: the sweep in NN-lane teams (hd_sweep_quad_kernel); HD_SWEEP_QUAD=0/1
+  int quad = 0;
   // true while a solve enqueues into a capturing stream: scratch may not grow then
   bool capturing = false;
   std::string err;
@@ -387,6 +389,7 @@ int hd_context_create(hd_context** out, int device) {
   hd_context* ctx = new hd_context();
   if (const char* e = std::getenv("HD_JACOBI_WARM")) ctx->warm = std::atoi(e) != 0;
   if (const char* e = std::getenv("HD_TEAM_SWEEP_LEAN")) ctx->lean = std::atoi(e) != 0;
+  if (const char* e = std::getenv("HD_SWEEP_QUAD")) ctx->quad = std::atoi(e) != 0;
   ctx->device = device;
   auto init = [ctx]() -> int {
     HD_HIP(ctx, hipSetDevice(ctx->device));
@@ -725,6 +728,7 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
     sa.nwave = in->nwave;
     sa.beam_scale = beam_in_sweep ? 1 : 0;
     sa.lean = ctx->lean;
+    sa.quad = ctx->quad;
     if (band && reg) {
       sa.wts = band->weight;
       sa.part = part;

@@ -24,6 +24,7 @@
 //   the vmcnt-ordered round trips of the one-wave-per-SIMD sweep)
 #include <cmath>
 #include <cstring>
+#include <utility>
 #include <vector>
 
 #include "hd_kernels.hpp"
@@ -804,6 +805,208 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
 }
 
 // ============================================================================
+// K2 for nstr 4 and 8 (NN = 2, 4) in NN-lane teams: the adding sweep of
+// hd_sweep_kernel with one solve per team, lane i holding row i of every NN x NN
+// matrix (A = Ra, R~, T~, W1, ZT, P) and element i of every vector; rows reach
+// the team's other lanes by DPP quad permutations (one v_mov_b64_dpp per element,
+// no LDS).  At these sizes the one-lane sweep is latency-bound -- a call of a few
+// hundred or thousand solves runs one or two waves per SIMD, each walking its
+// layers through dependent chains (C1 amars_lw: 16 solves, ~70 us of a ~120 us
+// step) -- and NN lanes per solve cut each lane's chain by ~NN and give the SIMDs
+// NN times the waves.  The pivot-free LU becomes a Gauss-Jordan elimination of
+// [W1 | T~ | v1] with the same pivots (lane i ends with row i of ZT = W1^-1 T~
+// and t1_i); records as the one-lane sweep (RecL in, RecB out), so the
+// back-substitution kernels are shared.
+// ============================================================================
+namespace {
+// lane k of this lane's NN-lane team (NN = 2: pairs, 4: quads) via quad_perm
+template <int NN, int K>
+__device__ __forceinline__ double qbc(double x) {
+  constexpr int ctrl = NN == 4 ? (K | (K << 2) | (K << 4) | (K << 6))
+                               : (K | (K << 2) | ((2 + K) << 4) | ((2 + K) << 6));
+  return __builtin_amdgcn_update_dpp(0.0, x, ctrl, 0xF, 0xF, true);
+}
+// sum over the team (a butterfly: every lane holds the same bits)
+template <int NN>
+__device__ __forceinline__ double qsum(double x) {
+  x += __builtin_amdgcn_update_dpp(0.0, x, 1 | (0 << 2) | (3 << 4) | (2 << 6), 0xF, 0xF, true);
+  if constexpr (NN == 4)
+    x += __builtin_amdgcn_update_dpp(0.0, x, 2 | (3 << 2) | (0 << 4) | (1 << 6), 0xF, 0xF, true);
+  return x;
+}
+template <int B, int E, class F, int... Is>
+__device__ __forceinline__ void qfor_impl(F&& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, B + Is>{}), ...);
+}
+template <int B, int E, class F>
+__device__ __forceinline__ void qfor(F&& f) {  // f(k), k = B .. E-1 (compile-time)
+  if constexpr (E > B) qfor_impl<B, E>(f, std::make_integer_sequence<int, E - B>{});
+}
+#define HD_Q(x) decltype(x)::value
+}  // namespace
+
+template <int NN>
+__global__ __launch_bounds__(64) void hd_sweep_quad_kernel(SweepArgs A) {
+  static_assert(NN == 2 || NN == 4, "pair / quad teams");
+  const Quad<NN>& Qc = quad<NN>();
+  const int lane = (int)threadIdx.x;
+  const int i = lane & (NN - 1);
+  const long slq = ((long)blockIdx.x * 64 + lane) / NN;
+  // a team past the chunk repeats the chunk's last solve and stores nothing: every
+  // lane of a quad takes part in its DPP exchanges
+  const bool valid = slq < A.nsc;
+  const long sl = valid ? slq : A.nsc - 1;
+  const long s = solve_of(A.s0 + sl, A.cmaj, A.nwave, A.ncol);
+  const int L = A.nlyr;
+  const size_t nsc = A.nsc;
+  using RL = RecL<NN>;
+  using RB = RecB<NN>;
+  int st = 0;
+
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
+  const double fb = A.fbeam ? A.fbeam[s] : 0.0;
+  const bool beam = fb > 0.0 && mu0 > 0.0;
+  const double alb = A.albedo ? A.albedo[s] : 0.0;
+  if (!(alb >= 0.0) || !(alb <= 1.0)) st |= kStBadInput;
+  double top = A.fisot ? A.fisot[s] : 0.0;
+  double bsurf = 0.0;
+  if (A.planck) {
+    bsurf = A.planckv[(size_t)(L + 1) * nsc + sl];
+    top += A.planckv[(size_t)(L + 2) * nsc + sl];
+  }
+  const double twopi = 2.0 * kPi;
+  const double rmu0 = beam ? 1.0 / mu0 : 0.0;
+  const double f0mu0 = beam ? fb * mu0 : 0.0;
+  const double g_i = Qc.g[i];
+  // record element e of this solve in a layer's record ([pair][nsc] of double2)
+  auto eoff = [&](int e) { return ((size_t)(e >> 1) * nsc + sl) * 2 + (e & 1); };
+
+  double ra[NN];  // row i of the reflection of the stack above
+#pragma unroll
+  for (int j = 0; j < NN; ++j) ra[j] = 0.0;
+  double sd = g_i * top;
+  double tauc = 0.0;
+
+  for (int lc = 0; lc < L; ++lc) {
+    const double* lb = A.scr + (size_t)lc * RL::pairs * nsc * 2;
+    double* bb = A.bsub + (size_t)lc * RB::pairs * nsc * 2;
+    double r[NN], tr[NN];
+#pragma unroll
+    for (int j = 0; j < NN; ++j) {
+      r[j] = lb[eoff(RL::R + sym_index<NN>(i, j))];
+      tr[j] = lb[eoff(RL::T + sym_index<NN>(i, j))];
+    }
+    const double eb = exp(-tauc * rmu0);
+    const double sscale = A.beam_scale ? eb : 1.0;
+    const double spl = lb[eoff(RL::Sp + i)] * sscale;
+    const double sml = lb[eoff(RL::Sm + i)] * sscale;
+    const double taup = lb[eoff(RL::Tau)];
+
+    // level lc (top of layer lc): F_dn = rc . I+ + cs  (A symmetric: column i = row i)
+    {
+      double rc = 0.0;
+#pragma unroll
+      for (int j = 0; j < NN; ++j) rc = fma(ra[j], Qc.g[j], rc);
+      const double cs = qsum<NN>(g_i * sd);
+      if (valid) {
+        bb[eoff(RB::Rc + i)] = twopi * rc;
+        if (i == 0) bb[eoff(RB::Cs)] = fma(twopi, cs, f0mu0 * eb);
+      }
+    }
+    // W1 = I - R A ; v1 = R Sd + S+
+    double w[NN];
+#pragma unroll
+    for (int j = 0; j < NN; ++j) w[j] = i == j ? 1.0 : 0.0;
+    double v = spl;
+    qfor<0, NN>([&](auto K) {
+      constexpr int k = HD_Q(K);
+#pragma unroll
+      for (int j = 0; j < NN; ++j) w[j] = fma(-r[k], qbc<NN, k>(ra[j]), w[j]);
+      v = fma(r[k], qbc<NN, k>(sd), v);
+    });
+    // Gauss-Jordan on [W1 | T~ | v1] (the one-lane sweep's LU pivots), rows
+    // normalised at the end: lane i ends with d_i [e_i | ZT_i | t1_i]
+    double z[NN], d = 1.0;
+#pragma unroll
+    for (int j = 0; j < NN; ++j) z[j] = tr[j];
+    qfor<0, NN>([&](auto K) {
+      constexpr int k = HD_Q(K);
+      const double pk = qbc<NN, k>(w[k]);
+      st |= fabs(pk) > 1.0e-12 ? 0 : kStPivot;
+      d = i == k ? pk : d;
+      const double f = i == k ? 0.0 : w[k] * rcp_nr(pk);
+      qfor<k + 1, NN>([&](auto J) { w[HD_Q(J)] = fma(-f, qbc<NN, k>(w[HD_Q(J)]), w[HD_Q(J)]); });
+#pragma unroll
+      for (int j = 0; j < NN; ++j) z[j] = fma(-f, qbc<NN, k>(z[j]), z[j]);
+      v = fma(-f, qbc<NN, k>(v), v);
+    });
+    {
+      const double rd = rcp_nr(d);
+#pragma unroll
+      for (int j = 0; j < NN; ++j) z[j] *= rd;  // row i of ZT
+      v *= rd;                                  // t1_i
+    }
+    if (valid) {
+#pragma unroll
+      for (int j = 0; j < NN; ++j) bb[eoff(RB::Z + j * NN + i)] = z[j];
+      bb[eoff(RB::Tv + i)] = v;
+    }
+    // u = A t1 + Sd ; P = A ZT ; Ra <- R + T P ; Sd <- T u + S-
+    double u = sd, p_[NN];
+#pragma unroll
+    for (int j = 0; j < NN; ++j) p_[j] = 0.0;
+    qfor<0, NN>([&](auto K) {
+      constexpr int k = HD_Q(K);
+      u = fma(ra[k], qbc<NN, k>(v), u);
+#pragma unroll
+      for (int j = 0; j < NN; ++j) p_[j] = fma(ra[k], qbc<NN, k>(z[j]), p_[j]);
+    });
+    double sdn = sml;
+#pragma unroll
+    for (int j = 0; j < NN; ++j) ra[j] = r[j];
+    qfor<0, NN>([&](auto K) {
+      constexpr int k = HD_Q(K);
+#pragma unroll
+      for (int j = 0; j < NN; ++j) ra[j] = fma(tr[k], qbc<NN, k>(p_[j]), ra[j]);
+      sdn = fma(tr[k], qbc<NN, k>(u), sdn);
+    });
+    sd = sdn;
+    tauc += taup;
+  }
+
+  // ---- Lambertian surface: I+ = g x ----
+  double rgi = 0.0;
+#pragma unroll
+  for (int j = 0; j < NN; ++j) rgi = fma(ra[j], Qc.g[j], rgi);
+  const double gsd = qsum<NN>(g_i * sd);
+  const double grg = qsum<NN>(g_i * rgi);
+  double esurf = (1.0 - alb) * bsurf;
+  const double dirsurf = f0mu0 * exp(-tauc * rmu0);
+  if (beam) esurf += alb * dirsurf / kPi;
+  const double x = (2.0 * alb * gsd + esurf) / (1.0 - 2.0 * alb * grg);
+  const double up = qsum<NN>(g_i * (g_i * x));
+  const double dn = qsum<NN>(g_i * fma(rgi, x, sd));
+  const double f0 = twopi * up, f1 = twopi * dn + dirsurf;
+  if (valid && i == 0) {
+    if (A.flux) {
+      double* fo = A.flux + (size_t)s * (L + 1) * 2;
+      fo[0] = f0;
+      fo[1] = f1;
+    }
+    if (A.fsurf) {
+      A.fsurf[sl] = f0;
+      A.fsurf[nsc + sl] = f1;
+    }
+    A.xsurf[sl] = x;
+  }
+  if (!isfinite(f0 + f1)) st |= kStNonFinite;
+  if (valid && st && i == 0) {
+    atomicOr(&A.status[s], st);
+    if (st & 0x0F) atomicOr(A.anyerr, 1);
+  }
+}
+
+// ============================================================================
 // K3: per-solve back-substitution bottom -> top.  Split from the adding sweep
 // so that it runs at the occupancy of its own small register footprint (the
 // sweep's register file allows one wave per SIMD): a pure stream over the
@@ -1150,16 +1353,28 @@ void launch_prologue(const PlanckArgs* pa, const TaucArgs* ta, hipStream_t strea
 }
 
 template <int NN>
+static void launch_sweep(const SweepArgs& sa, hipStream_t stream) {
+  if constexpr (NN == 2 || NN == 4) {
+    if (sa.quad) {  // NN-lane teams, one solve per team
+      hipLaunchKernelGGL(hd_sweep_quad_kernel<NN>, dim3((unsigned)((sa.nsc * NN + 63) / 64)),
+                         dim3(64), 0, stream, sa);
+      return;
+    }
+  }
+  hipLaunchKernelGGL(hd_sweep_kernel<NN>, dim3((unsigned)((sa.nsc + 63) / 64)), dim3(64), 0,
+                     stream, sa);
+}
+
+template <int NN>
 static hipError_t launch_chunk(const PlanckArgs* pa, const TaucArgs* ta, const LayerArgs& la,
                                const SweepArgs& sa, hipStream_t stream, hipEvent_t* ev) {
   launch_prologue(pa, ta, stream);
   const unsigned nb1 = (unsigned)(((la.nsc + 63) / 64) *
                                   ((la.nlyr + kLayersPerBlock - 1) / kLayersPerBlock));
-  const unsigned nb2 = (unsigned)((la.nsc + 63) / 64);
   if (ev) (void)hipEventRecord(ev[0], stream);
   hipLaunchKernelGGL(hd_layer_kernel<NN>, dim3(nb1), dim3(kLayerBlock), 0, stream, la);
   if (ev) (void)hipEventRecord(ev[1], stream);
-  hipLaunchKernelGGL(hd_sweep_kernel<NN>, dim3(nb2), dim3(64), 0, stream, sa);
+  launch_sweep<NN>(sa, stream);
   if (ev) (void)hipEventRecord(ev[2], stream);
   return hipGetLastError();
 }
@@ -1211,11 +1426,7 @@ static void launch_layer(const LayerArgs& la, hipStream_t stream) {
                                   ((la.nlyr + kLayersPerBlock - 1) / kLayersPerBlock));
   hipLaunchKernelGGL(hd_layer_kernel<NN>, dim3(nb1), dim3(kLayerBlock), 0, stream, la);
 }
-template <int NN>
-static void launch_sweep(const SweepArgs& sa, hipStream_t stream) {
-  hipLaunchKernelGGL(hd_sweep_kernel<NN>, dim3((unsigned)((sa.nsc + 63) / 64)), dim3(64), 0,
-                     stream, sa);
-}
+
 hipError_t launch_layer_nn(int nn, const LayerArgs& la, hipStream_t stream) {
   switch (nn) {
     case 1: launch_layer<1>(la, stream); break;

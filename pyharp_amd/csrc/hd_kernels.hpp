@@ -168,6 +168,8 @@ struct SweepArgs {
   // team path (nstr 18..32): the lean sweep (hd_team_mfma_sweep_lean_kernel, two waves
   // per SIMD) instead of the one-wave-per-SIMD sweep
   int lean;
+  // register path, nstr 4 / 8: the sweep in NN-lane teams (hd_sweep_quad_kernel)
+  int quad;
 };
 
 // chunk epilogue of the fused band sum: bflux[c] (=|+=) sum of the chunk's
