@@ -41,11 +41,13 @@ struct hd_context {
   // team-path Jacobi from the tabulated (ssa, chi_1) eigenvectors
   // (hd_kernels.hpp); HD_JACOBI_WARM=0 in the environment turns it off (A/B)
   int warm = 1;
-  // team path: the two-waves-per-SIMD sweep (hd_team_mfma_sweep_lean_kernel);
-  // HD_TEAM_SWEEP_LEAN=0/1 in the environment picks it when a context is created
-  int lean = 0;
-  // nstr 4 / 8: the sweep in NN-lane teams (hd_sweep_quad_kernel); HD_SWEEP_QUAD=0/1
-  int quad = 0;
+  // team path: the two-waves-per-SIMD sweep (hd_team_mfma_sweep_lean_kernel, the
+  // default); HD_TEAM_SWEEP_LEAN=0 in the environment picks the one-wave sweep when
+  // a context is created
+  int lean = 1;
+  // nstr 4 / 8: the sweep in NN-lane teams (hd_sweep_quad_kernel) for chunks of at
+  // most kQuadMaxSolves solves (-1, the default), always (1) or never (0): HD_SWEEP_QUAD
+  int quad = -1;
   // true while a solve enqueues into a capturing stream: scratch may not grow then
   bool capturing = false;
   std::string err;
@@ -389,7 +391,7 @@ int hd_context_create(hd_context** out, int device) {
   hd_context* ctx = new hd_context();
   if (const char* e = std::getenv("HD_JACOBI_WARM")) ctx->warm = std::atoi(e) != 0;
   if (const char* e = std::getenv("HD_TEAM_SWEEP_LEAN")) ctx->lean = std::atoi(e) != 0;
-  if (const char* e = std::getenv("HD_SWEEP_QUAD")) ctx->quad = std::atoi(e) != 0;
+  if (const char* e = std::getenv("HD_SWEEP_QUAD")) ctx->quad = std::atoi(e) < 0 ? -1 : std::atoi(e) != 0;
   ctx->device = device;
   auto init = [ctx]() -> int {
     HD_HIP(ctx, hipSetDevice(ctx->device));

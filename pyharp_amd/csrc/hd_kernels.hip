@@ -1355,7 +1355,7 @@ void launch_prologue(const PlanckArgs* pa, const TaucArgs* ta, hipStream_t strea
 template <int NN>
 static void launch_sweep(const SweepArgs& sa, hipStream_t stream) {
   if constexpr (NN == 2 || NN == 4) {
-    if (sa.quad) {  // NN-lane teams, one solve per team
+    if (sa.quad > 0 || (sa.quad < 0 && sa.nsc <= kQuadMaxSolves)) {  // NN-lane teams
       hipLaunchKernelGGL(hd_sweep_quad_kernel<NN>, dim3((unsigned)((sa.nsc * NN + 63) / 64)),
                          dim3(64), 0, stream, sa);
       return;

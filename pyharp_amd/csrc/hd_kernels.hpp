@@ -132,6 +132,12 @@ struct LayerArgs {
   int warm;      // team path: start the Jacobi from the (ssa, chi_1) bin's eigenvectors
 };
 
+// Up to this many solves per chunk the nstr 4 / 8 sweep runs in NN-lane teams: there
+// the one-lane sweep leaves most SIMDs idle or at one wave (C1 16 solves, C3 19 990:
+// +25 % and +9 % a step); at 1e5 solves it fills the chip and the teams' redundant
+// work (2x the one-lane flops) cancels their shorter chains (C3l within noise).
+constexpr int kQuadMaxSolves = 32768;
+
 struct SweepArgs {
   const double* scr;
   double* bsub;
@@ -168,7 +174,8 @@ struct SweepArgs {
   // team path (nstr 18..32): the lean sweep (hd_team_mfma_sweep_lean_kernel, two waves
   // per SIMD) instead of the one-wave-per-SIMD sweep
   int lean;
-  // register path, nstr 4 / 8: the sweep in NN-lane teams (hd_sweep_quad_kernel)
+  // register path, nstr 4 / 8: the sweep in NN-lane teams (hd_sweep_quad_kernel):
+  // 1 on, 0 off, -1 for chunks of at most kQuadMaxSolves solves
   int quad;
 };
 
