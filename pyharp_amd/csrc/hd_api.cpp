@@ -575,13 +575,16 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
   // `lay` stream beside chunk k's sweep on the caller's stream
   const bool team_pipe = !reg && nsolve > chunk;
   const bool beam = in->fbeam != nullptr;
-  // Register path without Planck emission: the layer kernel's beam sources are for
-  // a unit beam at the layer top and the sweep scales them by exp(-tau_c/mu0) from
-  // its own running depth, so no chunk needs the cumulative-depth prologue -- which
-  // sat on the side stream behind the previous back-substitution and held each
-  // chunk's layer kernel back until the sweep beside it was done.  With Planck the
-  // sources mix beam and thermal terms and the prologue stays.
-  const bool beam_in_sweep = reg && beam && !planck;
+  // Without Planck emission the layer kernels' beam sources are for a unit beam at
+  // the layer top and the sweep scales them by exp(-tau_c/mu0) from its own running
+  // depth, so no chunk needs the cumulative-depth prologue.  Register path: it sat
+  // on the side stream behind the previous back-substitution and held each chunk's
+  // layer kernel back until the sweep beside it was done.  Team path: chunk k+1's
+  // prologue, launched as chunk k's sweep, waited for SIMDs the sweep's two
+  // 254-register waves hold (up to 3.3 ms of a 48 ms C5 step,
+  // profiles/r04/c5_timeline_last_step_v2.txt).  With Planck the sources mix beam
+  // and thermal terms and the prologue stays.
+  const bool beam_in_sweep = beam && !planck;
   const bool need_tauc = beam && !beam_in_sweep;
   const bool need_pro = planck || need_tauc;
   const int nb = 2;  // buffers of the per-chunk regions (two chunks in flight)

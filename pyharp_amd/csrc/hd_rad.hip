@@ -25,6 +25,8 @@
 // Formulation: DESIGN.md section 3b, mirrored in numpy by
 // tests/kernel_model_rad.py; oracle: oracle/disort_rad_np.py.
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 
 #include "hd_rad.hpp"
 
@@ -170,48 +172,6 @@ __device__ __forceinline__ void flag(const RadArgs& A, long s, int st) {
   }
 }
 
-// int_{t1}^{t2} a exp(-c (t - tref)) exp(-(t - t1)/mu) dt/mu, t1 = evaluation
-// depth, (t2 - t1)/mu >= 0; the 1 + c mu -> 0 limit through (1 - e^-x)/x
-__device__ __forceinline__ double seg_exp(double a, double c, double t1, double t2, double tref,
-                                          double mu) {
-  const double p1 = exp(-c * (t1 - tref));
-  const double den = fma(c, mu, 1.0);
-  const double dt = (t2 - t1) / mu;
-  const double x = den * dt;
-  if (fabs(x) < 0.5) {
-    const double ph = x == 0.0 ? 1.0 : -expm1(-x) / x;
-    return a * p1 * dt * ph;
-  }
-  const double p2 = exp(-c * (t2 - tref) - dt);
-  return a * (p1 - p2) / den;
-}
-
-// (pa - pb)/den where pb = pa e^{-y}, y = den * len: the direct quotient, or
-// pa * len * (1 - e^-y)/y by its Taylor series when |y| < 1/2 (den -> 0)
-__device__ __forceinline__ double dexp(double pa, double pb, double den, double len) {
-  const double y = den * len;
-  // sum_{n<=13} (-y)^n/(n+1)!: |y|^14/15! < 5e-17 for |y| < 1/2
-  double ph = 1.0 / 87178291200.0;  // 1/14!
-  ph = fma(ph, -y, 1.0 / 6227020800.0);
-  ph = fma(ph, -y, 1.0 / 479001600.0);
-  ph = fma(ph, -y, 1.0 / 39916800.0);
-  ph = fma(ph, -y, 1.0 / 3628800.0);
-  ph = fma(ph, -y, 1.0 / 362880.0);
-  ph = fma(ph, -y, 1.0 / 40320.0);
-  ph = fma(ph, -y, 1.0 / 5040.0);
-  ph = fma(ph, -y, 1.0 / 720.0);
-  ph = fma(ph, -y, 1.0 / 120.0);
-  ph = fma(ph, -y, 1.0 / 24.0);
-  ph = fma(ph, -y, 1.0 / 6.0);
-  ph = fma(ph, -y, 0.5);
-  ph = fma(ph, -y, 1.0);
-  return fabs(y) < 0.5 ? pa * len * ph : (pa - pb) / den;
-}
-
-// user depth lu of solve sl: the caller's utau or the level depths
-__device__ __forceinline__ double user_tau(const RadArgs& A, int lu, int sl) {
-  return A.utau ? A.utau[lu] : A.taus[(size_t)lu * A.ns + sl];
-}
 
 }  // namespace
 
@@ -1556,6 +1516,15 @@ hipError_t upload_rad_tables(const QuadHost* per_nn) {
   return hipMemcpyToSymbol(HIP_SYMBOL(c_rad), &c, sizeof(RadConst));
 }
 
+// HD_RAD_USER=rolled: nstr 18..32 user angles by the one-lane-per-(unit, angle) kernel
+static bool rad_user_rolled() {
+  static const bool v = [] {
+    const char* e = std::getenv("HD_RAD_USER");
+    return e && std::strcmp(e, "rolled") == 0;
+  }();
+  return v;
+}
+
 template <int NN>
 static void launch_rad(const RadArgs& a, bool radiances, hipStream_t st) {
   const unsigned ns_b = (unsigned)((a.ns + 255) / 256);
@@ -1579,8 +1548,11 @@ static void launch_rad(const RadArgs& a, bool radiances, hipStream_t st) {
                      a);
   if (radiances && a.numu > 0 && a.nphi > 0) {
     const long nr = (long)a.ns * a.numu;
-    hipLaunchKernelGGL(hd_rad_user_kernel<NN>, dim3((unsigned)((nr + 63) / 64), (unsigned)a.nm),
-                       dim3(64), 0, st, a);
+    if (NN > kMaxRegNN && a.numu <= rad_layer_record_doubles(NN) && !rad_user_rolled())
+      (void)hd::launch_rad_team_user(NN, a, st);  // team layout + MFMA (hd_team_mfma.hip)
+    else
+      hipLaunchKernelGGL(hd_rad_user_kernel<NN>, dim3((unsigned)((nr + 63) / 64), (unsigned)a.nm),
+                         dim3(64), 0, st, a);
     const long na = (long)a.ns * a.nphi * a.ntau * a.numu;
     hipLaunchKernelGGL(hd_rad_azimuth_kernel, dim3((unsigned)((na + 255) / 256)), dim3(256), 0,
                        st, a);

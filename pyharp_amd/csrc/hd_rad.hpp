@@ -71,6 +71,49 @@ struct RadArgs {
   int corint;  // Nakajima-Tanaka TMS correction of the single scattering
 };
 
+// int_{t1}^{t2} a exp(-c (t - tref)) exp(-(t - t1)/mu) dt/mu, t1 = evaluation
+// depth, (t2 - t1)/mu >= 0; the 1 + c mu -> 0 limit through (1 - e^-x)/x
+__device__ __forceinline__ double seg_exp(double a, double c, double t1, double t2, double tref,
+                                          double mu) {
+  const double p1 = exp(-c * (t1 - tref));
+  const double den = fma(c, mu, 1.0);
+  const double dt = (t2 - t1) / mu;
+  const double x = den * dt;
+  if (fabs(x) < 0.5) {
+    const double ph = x == 0.0 ? 1.0 : -expm1(-x) / x;
+    return a * p1 * dt * ph;
+  }
+  const double p2 = exp(-c * (t2 - tref) - dt);
+  return a * (p1 - p2) / den;
+}
+
+// (pa - pb)/den where pb = pa e^{-y}, y = den * len: the direct quotient, or
+// pa * len * (1 - e^-y)/y by its Taylor series when |y| < 1/2 (den -> 0)
+__device__ __forceinline__ double dexp(double pa, double pb, double den, double len) {
+  const double y = den * len;
+  // sum_{n<=13} (-y)^n/(n+1)!: |y|^14/15! < 5e-17 for |y| < 1/2
+  double ph = 1.0 / 87178291200.0;  // 1/14!
+  ph = fma(ph, -y, 1.0 / 6227020800.0);
+  ph = fma(ph, -y, 1.0 / 479001600.0);
+  ph = fma(ph, -y, 1.0 / 39916800.0);
+  ph = fma(ph, -y, 1.0 / 3628800.0);
+  ph = fma(ph, -y, 1.0 / 362880.0);
+  ph = fma(ph, -y, 1.0 / 40320.0);
+  ph = fma(ph, -y, 1.0 / 5040.0);
+  ph = fma(ph, -y, 1.0 / 720.0);
+  ph = fma(ph, -y, 1.0 / 120.0);
+  ph = fma(ph, -y, 1.0 / 24.0);
+  ph = fma(ph, -y, 1.0 / 6.0);
+  ph = fma(ph, -y, 0.5);
+  ph = fma(ph, -y, 1.0);
+  return fabs(y) < 0.5 ? pa * len * ph : (pa - pb) / den;
+}
+
+// user depth lu of solve sl: the caller's utau or the level depths
+__device__ __forceinline__ double user_tau(const RadArgs& A, int lu, int sl) {
+  return A.utau ? A.utau[lu] : A.taus[(size_t)lu * A.ns + sl];
+}
+
 hipError_t upload_rad_tables(const QuadHost* per_nn);  // nn 1..kRadMaxNN
 // tauc/planck prologue must have run (launch_prologue) for the chunk's solves;
 // radiances = false: fluxes at the user depths only (mode 0, no uu)
@@ -82,6 +125,12 @@ hipError_t launch_rad_team_sweep(int nn, const RadArgs& a, hipStream_t stream);
 // nstr 18..32: the per-(unit, layer) setup on the team layout + FP64 MFMA, and its
 // Y_l^m tables (uploaded with the other intensity-path tables)
 hipError_t launch_rad_team_layer(int nn, const RadArgs& a, hipStream_t stream);
+// nstr 18..32: the user-angle integration in two kernels -- per (unit, layer) on the
+// team layout + FP64 MFMA (every user angle's whole-layer source term and the
+// interior user depths' partial integrals), then a per-(unit, angle) scan over the
+// layers.  Needs numu <= rad_layer_record_doubles(nn) (the whole-layer terms reuse
+// the layer-operator records, free after the sweep)
+hipError_t launch_rad_team_user(int nn, const RadArgs& a, hipStream_t stream);
 hipError_t upload_rad_tables_team(const QuadHost* per_nn);
 // nstr 18..32: the same kernels compiled with rolled NN-loops (hd_rad_wide.hip)
 namespace wide {

@@ -245,7 +245,8 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_layer_kernel(LayerArgs A) 
       double yy = sd_i * mu_i * sv;
       team_lsolve<NN>(lch, rdl, yy);
       team_usolve<NN>(lt, rdl, yy);
-      const double tauc = A.tauc[(size_t)lc * A.nsc + sl];
+      // tauc null: sources for a unit beam at the layer top (the sweep scales them)
+      const double tauc = A.tauc ? A.tauc[(size_t)lc * A.nsc + sl] : 0.0;
       const double att = 0.5 * exp(-tauc * rmu0);
       const double dd = rg_i * fma(-yy, rmu0, lxd);
       zp = (sv + dd) * att;
@@ -383,8 +384,11 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_sweep_kernel(SweepArgs A) 
     double* bw = act ? bp : A.sink;  // lanes >= NN store into the sink (no branches)
     double rl[NN];
     sfor<0, NN>([&](auto J) { rl[HD_K(J)] = rec[ii * NN + HD_K(J)] * msk; });
-    const double spl = rec[2 * NN * NN + ii] * msk;
-    const double sml = rec[2 * NN * NN + NN + ii] * msk;
+    // direct beam at the layer top; a unit-beam record's sources scale with it
+    const double eb = exp(-tauc * rmu0);
+    const double sscale = A.beam_scale ? eb : 1.0;
+    const double spl = rec[2 * NN * NN + ii] * msk * sscale;
+    const double sml = rec[2 * NN * NN + NN + ii] * msk * sscale;
 
     // level lc (top of layer lc): F_dn = rc . I+ + cs
     {
@@ -392,7 +396,7 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_sweep_kernel(SweepArgs A) 
       sfor<0, NN>([&](auto J) { t = fma(ra[HD_K(J)], Qc.g[HD_K(J)], t); });
       bw[NN * NN + NN + ii] = twopi * t;
       const double cs = team_sum(g_i * sd);
-      if (i == 0) bp[NN * NN + 2 * NN] = fma(twopi, cs, f0mu0 * exp(-tauc * rmu0));
+      if (i == 0) bp[NN * NN + 2 * NN] = fma(twopi, cs, f0mu0 * eb);
     }
     // W1 = I - R_l A ; t1 = R_l Sd + S+
     double w[NN];

@@ -457,7 +457,8 @@ __global__ __launch_bounds__(64, 2) void hd_team_mfma_layer_kernel(LayerArgs A) 
       const double sv = team_matvec<NN>(r_, ttv) * rg_i;
       get_rows<NN>(S0, t, i, r_);
       const double yy = team_matvec<NN>(r_, sd_i * mu_i * sv);
-      const double tauc = A.tauc[(size_t)lc * A.nsc + sl];
+      // tauc null: sources for a unit beam at the layer top (the sweep scales them)
+      const double tauc = A.tauc ? A.tauc[(size_t)lc * A.nsc + sl] : 0.0;
       const double att = 0.5 * exp(-tauc * rmu0);
       const double dd = rg_i * fma(-yy, rmu0, lxd);
       zp = (sv + dd) * att;
@@ -654,8 +655,11 @@ __global__ __launch_bounds__(64, 1) void hd_team_mfma_sweep_kernel(SweepArgs A) 
       rl[HD_K(J)] = rec[ii * NN + HD_K(J)] * msk;
       tr[HD_K(J)] = rec[NN * NN + ii * NN + HD_K(J)] * msk;
     });
-    const double spl = rec[2 * NN * NN + ii] * msk;
-    const double sml = rec[2 * NN * NN + NN + ii] * msk;
+    // direct beam at the layer top; a unit-beam record's sources scale with it
+    const double eb = exp(-tauc * rmu0);
+    const double sscale = A.beam_scale ? eb : 1.0;
+    const double spl = rec[2 * NN * NN + ii] * msk * sscale;
+    const double sml = rec[2 * NN * NN + NN + ii] * msk * sscale;
 
     // level lc (top of layer lc): F_dn = rc . I+ + cs
     {
@@ -663,7 +667,7 @@ __global__ __launch_bounds__(64, 1) void hd_team_mfma_sweep_kernel(SweepArgs A) 
       sfor<0, NN>([&](auto J) { tq = fma(ra[HD_K(J)], Qc.g[HD_K(J)], tq); });
       bw[NN * NN + NN + ii] = twopi * tq;
       const double cs = team_sum(g_i * sd);
-      if (i == 0 && valid) bp[NN * NN + 2 * NN] = fma(twopi, cs, f0mu0 * exp(-tauc * rmu0));
+      if (i == 0 && valid) bp[NN * NN + 2 * NN] = fma(twopi, cs, f0mu0 * eb);
     }
     // W1 = I - R A on the matrix core, to team rows through LDS
     {
@@ -931,7 +935,10 @@ __global__ __launch_bounds__(64, 2) void hd_team_mfma_sweep_lean_kernel(SweepArg
     const double* rec = A.scr + ((size_t)lc * nsc + sl) * ne1t<NN>();
     double* bp = A.bsub + ((size_t)lc * nsc + sl) * ne2t<NN>();
     double* bw = (act && valid) ? bp : A.sink;
-    const double spl = rec[2 * NN * NN + ii] * msk;
+    // direct beam at the layer top; a unit-beam record's sources scale with it
+    const double eb = exp(-tauc * rmu0);
+    const double sscale = A.beam_scale ? eb : 1.0;
+    const double spl = rec[2 * NN * NN + ii] * msk * sscale;
 
     // level lc (top of layer lc): F_dn = rc . I+ + cs; A's row i from S0
     {
@@ -941,7 +948,7 @@ __global__ __launch_bounds__(64, 2) void hd_team_mfma_sweep_lean_kernel(SweepArg
       sfor<0, NN>([&](auto J) { tq = fma(ar[HD_K(J)] * msk, Qc.g[HD_K(J)], tq); });
       bw[NN * NN + NN + ii] = twopi * tq;
       const double cs = team_sum(g_i * sd);
-      if (i == 0 && valid) bp[NN * NN + 2 * NN] = fma(twopi, cs, f0mu0 * exp(-tauc * rmu0));
+      if (i == 0 && valid) bp[NN * NN + 2 * NN] = fma(twopi, cs, f0mu0 * eb);
     }
     // W1 = I - R A on the matrix core, to team rows through S1
     double w[NN];
@@ -1030,7 +1037,7 @@ __global__ __launch_bounds__(64, 2) void hd_team_mfma_sweep_lean_kernel(SweepArg
     {
       double tr[NN];
       load_row(rec, NN * NN, tr);
-      double tq = rec[2 * NN * NN + NN + ii] * msk;
+      double tq = rec[2 * NN * NN + NN + ii] * msk * sscale;
       sfor<0, NN>([&](auto K) { tq = fma(tr[HD_K(K)], bc<HD_K(K)>(u), tq); });
       sd = tq * msk;
     }
@@ -1845,6 +1852,465 @@ hipError_t launch_team_layer_mfma(int nn, const LayerArgs& la, hipStream_t strea
   }
 }
 
+
+// ============================================================================
+// Intensity path, nstr 18..32: the user-angle source-function integration
+// (hd_rad.hip's hd_rad_user_kernel, c_usrint) in two kernels.
+//
+// hd_rad_team_user_kernel: one wave = four (unit, layer) problems.  The mode-m
+// phase row at a user angle enters only through H(+-k) = c_e X +- c_o Y (DESIGN.md
+// section 3b), linear in the angle's Y_l^m row, so per problem the two maps
+//     P^T = diag(sd) L V,   Q^T = -diag(sd) L^-T V K
+// are formed once on the matrix core and applied to eight user angles at a time:
+// [ce | cx] = [P | Q] . blockdiag(C_e, C_o), a 16 x 16 x 32 product whose B operand
+// (the angles' c_e/c_o columns, lane (h, c): angle c & 7, parity c >> 3, rows
+// h + 4s) each lane builds from the Y_l^m recurrences -- instead of one lane per
+// (unit, angle) streaming L and V and solving with L for every angle (private
+// memory at NN 9..16: 60 % of the nstr-32 radiance time, profiles/r03/rad/).
+// Each lane then sums its four eigen-terms of the whole-layer integral (the
+// decaying and the 1 - k|mu| -> 0 family through dexp), the team sums go through
+// LDS, and 32 lanes add the beam and thermal terms: the layer's source term
+// "lay" per (unit, angle) -> rsw (free after the sweep), and for user depths
+// strictly inside the layer the partial integral from the depth to the ray's
+// entry -> radm.
+// hd_rad_team_user_scan_kernel: one lane per (unit, angle): the boundary value,
+// then I_exit = I_entry e^{-tau'/|mu|} + lay layer by layer along the ray, the
+// radiance at each user depth (interior: I_entry e^{-|t_in - t|/|mu|} + partial).
+// ============================================================================
+template <int NN>
+__global__ __launch_bounds__(64, 2) void hd_rad_team_user_kernel(RadArgs A) {
+  __shared__ double lds[2 * kSet + 8 * 32 + 8 * 4 + 8 * 8];
+  double* S0 = lds;          // rows of L^-T
+  double* S1 = lds + kSet;   // rows of L
+  constexpr int N = 2 * NN;
+  constexpr int nsym = NN * (NN + 1) / 2;
+  constexpr int NE1 = rad_layer_record_doubles(NN);
+  constexpr int NR = rad_rec_doubles(NN);
+  constexpr int oV = nsym, oK = nsym + NN * NN, oZp = oK + NN, oZm = oZp + NN, oH = oZm + NN;
+  constexpr int oBt = oH + NN, oSl = oBt + 1, oTp = oSl + 1, oOm = oTp + 1, oEk = oOm + 1;
+  constexpr int oE0 = oEk + NN;
+  const Quad<NN>& Qc = tquad<NN>(c_qt);
+  const int lane = (int)threadIdx.x;
+  const int h = lane >> 4, c = lane & 15;  // M layout
+  const int t = h, i = c;                  // T layout: team t, row i
+  const bool act = i < NN;
+  const int ii = act ? i : 0;
+  const int L = A.nlyr;
+  const size_t nu = A.nu;
+  const int grp = block_group(L);
+  const int lc = block_layer(L);
+  int um[4];
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt) um[tt] = grp * 4 + tt < A.nu ? grp * 4 + tt : grp * 4;
+  const double* rec = A.rrd + (size_t)lc * NR * nu;  // element e of unit v: rec[e * nu + v]
+  auto rv = [&](int e, int tt) { return rec[(size_t)e * nu + um[tt]]; };
+
+  for (int k = lane; k < 2 * kSet; k += 64) lds[k] = 0.0;
+  lds_fence();
+
+  // ---- L's rows (T layout) and L^-T's rows by the team's forward substitution ----
+  {
+    const int u = um[t];
+    const int r0 = ii * (ii + 1) / 2;
+    double lrow[NN];
+    sfor<0, NN>([&](auto K) {
+      constexpr int k = HD_K(K);
+      lrow[k] = (act && k <= ii) ? rec[(size_t)(r0 + (k <= ii ? k : 0)) * nu + u] : 0.0;
+    });
+    double rdl = act ? 1.0 / rec[(size_t)(r0 + ii) * nu + u] : 0.0;
+    double z[NN];
+    team_tri_inverse_col<NN>(lrow, rdl, z);  // row i of L^-T
+    put_rows<NN>(S0, t, i, z);
+    put_rows<NN>(S1, t, i, lrow);
+  }
+  lds_fence();
+  lds_fence();
+  // ---- per problem: the layer's delta-M scalars (c_setdis, as hd_rad_user_kernel) ----
+  int mt[4];
+  double ft[4], rft[4], taupt[4];
+  const double* qt[4];
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt) {
+    mt[tt] = um[tt] / A.ns;
+    const int sl = um[tt] - mt[tt] * A.ns;
+    qt[tt] = A.prop + ((size_t)(A.s0 + sl) * L + (L - 1 - lc)) * A.nprop;
+    double ssa = A.nprop > 1 ? qt[tt][1] : 0.0;
+    if (ssa == 1.0) ssa = 1.0 - kDither;
+    const double f = A.nmom >= N ? qt[tt][1 + N] : 0.0;
+    const double om = ssa * (1.0 - f) / (1.0 - ssa * f);
+    ft[tt] = f;
+    rft[tt] = om / (1.0 - f);
+    taupt[tt] = rv(oTp, tt);
+  }
+  double* red = lds + 2 * kSet;  // [angle][lay | sc | x0 | th][h, parity]
+  double* aux = red + 8 * 32;     // [angle][ab | a0 | a1t | -]
+  double* red2 = aux + 8 * 4;     // [angle][h, parity]
+  const int a = c & 7, fam = c >> 3;
+  const int nmom = A.nmom;
+
+  for (int ab0 = 0; ab0 < A.numu; ab0 += 8) {
+    // the units laundered per angle block: the record loads below are then issued
+    // where they are used instead of all being hoisted out of this loop (192 VGPRs)
+    int uml[4];
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      uml[tt] = um[tt];
+      asm volatile("" : "+s"(uml[tt]));
+    }
+    auto rl = [&](int e, int tt) { return rec[(size_t)e * nu + uml[tt]]; };
+    const int iu = ab0 + a;
+    const bool aok = iu < A.numu;
+    const double muu = aok ? A.umu[iu] : 1.0;
+    const bool up = muu > 0.0;
+    const double anu = fabs(muu);
+    const double sxu = sqrt(fmax(0.0, 1.0 - muu * muu));
+    // one problem at a time (compile-time tt: its PT/QT registers), fenced so that
+    // only PT, QT and this problem's values are live
+    sfor<0, 4>([&](auto TT) {
+      constexpr int tt = HD_K(TT);
+      asm volatile("" : "+s"(uml[tt]));  // this problem's loads stay in its phase
+      const int v = grp * 4 + tt;  // this problem's unit (>= nu: a repeat, not stored)
+      const int m = mt[tt];
+      const int sl = um[tt] - m * A.ns;
+      const long s = A.s0 + sl;
+      const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
+      const double fb = A.fbeam ? A.fbeam[s] : 0.0;
+      const bool beam = fb > 0.0 && mu0 > 0.0;
+      const double rmu0 = beam ? 1.0 / mu0 : 0.0;
+      const bool therm = A.planck && m == 0;
+      const double taup = taupt[tt];
+      // ---- this lane's rows of the angle's c_e (c < 8) or c_o (c >= 8) column, and
+      // its share of x0 = sum_l g_l Y_l^m(mu) Y_l^m(-mu0) ----
+      double cu[4] = {0.0, 0.0, 0.0, 0.0};
+      double xp = 0.0;
+      {
+        const int lpar = (m & 1) ^ fam;  // this lane's parity of l
+        const double mub = beam ? mu0 : 0.0;
+        const double sx0 = sqrt(fmax(0.0, 1.0 - mub * mub));
+        const double* lam = rad_lam<NN>(m);
+        double su = c_rtt.seed[m], s0v = su;
+        for (int k = 0; k < m; ++k) {
+          su *= sxu;
+          s0v *= sx0;
+        }
+        double y1u = 0.0, y2u = 0.0, y10 = 0.0, y20 = 0.0;
+        const double* q = qt[tt];
+        const double f = ft[tt], rf = rft[tt];
+#pragma nounroll
+        for (int l2 = 0; l2 < NN; ++l2) {
+          double yv = 0.0, y0v = 0.0;
+#pragma unroll
+          for (int p = 0; p < 2; ++p) {
+            const int l = 2 * l2 + p;
+            const double cra = c_rtt.ra[m][l], crb = c_rtt.rb[m][l];
+            const double yu = l < m ? 0.0 : (l == m ? su : fma(cra * muu, y1u, -crb * y2u));
+            const double y0 = l < m ? 0.0 : (l == m ? s0v : fma(cra * mub, y10, -crb * y20));
+            y2u = y1u;
+            y1u = yu;
+            y20 = y10;
+            y10 = y0;
+            yv = p == lpar ? yu : yv;
+            y0v = p == lpar ? y0 : y0v;
+          }
+          const int l = 2 * l2 + lpar;
+          const double chi = l == 0 ? 1.0 : (l <= nmom ? q[1 + l] : 0.0);
+          const double gl = (2 * l + 1) * (chi - f) * rf;
+          const double gy = 0.5 * gl * yv;
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) {
+            const int r = h + 4 * s4;
+            cu[s4] = fma(gy, r < NN ? lam[l * NN + (r < NN ? r : 0)] : 0.0, cu[s4]);
+          }
+          const double y0s = ((l + m) & 1) ? -y0v : y0v;
+          xp = fma((l2 & 3) == h ? gl * yv : 0.0, y0s, xp);
+        }
+      }
+      // ---- P^T = diag(sd) L V and Q^T = -diag(sd) L^-T V K, this problem's M layout
+      // (the A^T operand of the next product) ----
+      double PT[4], QT[4];
+      {
+        double vm[4], x[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = h + 4 * q;
+          const bool in = r < NN && c < NN;
+          vm[q] = in ? rl(oV + (in ? r * NN + c : 0), tt) : 0.0;
+        }
+        d4 p = {0.0, 0.0, 0.0, 0.0}, g = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q] = S1[tt * kTile + c * kS + h + 4 * q];  // L^T (M)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) p = __builtin_amdgcn_mfma_f64_16x16x4f64(x[s4], vm[s4], p, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q] = S0[tt * kTile + c * kS + h + 4 * q];  // L^-1 (M)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) g = __builtin_amdgcn_mfma_f64_16x16x4f64(x[s4], vm[s4], g, 0, 0, 0);
+        const double kc = c < NN ? rl(oK + (c < NN ? c : 0), tt) : 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = h + 4 * q;
+          const double sdr = r < NN ? Qc.sd[r < NN ? r : 0] : 0.0;
+          PT[q] = p[q] * sdr;
+          QT[q] = g[q] * (-kc * sdr);
+        }
+      }
+      // ---- [ce | cx] = [P | Q] . blockdiag(C_e, C_o) on the matrix core ----
+      d4 hacc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+        hacc = __builtin_amdgcn_mfma_f64_16x16x4f64(PT[s4], fam == 0 ? cu[s4] : 0.0, hacc, 0, 0, 0);
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+        hacc = __builtin_amdgcn_mfma_f64_16x16x4f64(QT[s4], fam == 1 ? cu[s4] : 0.0, hacc, 0, 0, 0);
+      // ---- this lane's four eigen-terms of the whole-layer integral; beam/thermal sums ----
+      const double lmu = taup / anu;
+      const double emu = exp(-lmu);
+      double amp[4], kq[4];
+      double lp = 0.0, sc = 0.0, th = 0.0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = h + 4 * q;
+        const bool jok = j < NN;
+        const int jj = jok ? j : 0;
+        // lane c holds ce (c < 8) or cx (c >= 8) of angle c & 7; its partner c ^ 8 the other
+        const double own = hacc[q];
+        const double oth = xperm<8>(own);
+        const double ce = fam ? oth : own, cx = fam ? own : oth;
+        const double cc = jok ? A.cst[((size_t)lc * 2 * NN + fam * NN + jj) * nu + uml[tt]] : 0.0;
+        const double am = cc * (fam ? ce - cx : ce + cx);  // hpl_j (c < 8), hmi_j (c >= 8)
+        const double kj = jok ? rl(oK + jj, tt) : 0.0;
+        const double ek = jok ? rl(oEk + jj, tt) : 1.0;
+        // hpl's +k family decays along upward rays, hmi's along downward ones; the
+        // other meets 1 - k|mu| -> 0
+        const bool dec = (fam == 0) == up;
+        const double term = dec ? dexp(1.0, ek * emu, fma(kj, anu, 1.0), lmu)
+                                : dexp(ek, emu, fma(-kj, anu, 1.0), lmu);
+        lp = fma(am, term, lp);
+        amp[q] = am;
+        kq[q] = kj;
+        const double wi = jok ? Qc.w[jj] : 0.0;
+        const double zp = jok ? rl(oZp + jj, tt) : 0.0, zm = jok ? rl(oZm + jj, tt) : 0.0;
+        const double hr = jok ? rl(oH + jj, tt) : 0.0;
+        sc = fma(wi * cu[q], fam ? zp - zm : zp + zm, sc);
+        th = fma(wi, cu[q] * (fam ? hr : 1.0), th);
+      }
+      {
+        double* rp = red + a * 32 + h * 2 + fam;
+        rp[0] = lp;
+        rp[8] = sc;
+        rp[16] = xp;
+        rp[24] = th;
+      }
+      lds_fence();
+      // ---- lanes 0..7, one per angle: team sums, the beam and thermal terms; lay -> rsw ----
+      if (lane < 8) {
+        const int iv = ab0 + lane;
+        const double* rp = red + lane * 32;
+        double lay = 0.0, scs = 0.0, x0 = 0.0, we = 0.0, wo = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          lay += rp[k];
+          scs += rp[8 + k];
+          x0 += rp[16 + k];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          we += rp[24 + 2 * k];
+          wo += rp[25 + 2 * k];
+        }
+        const double mv = iv < A.numu ? A.umu[iv] : 1.0;
+        const bool upv = mv > 0.0;
+        const double av = fabs(mv);
+        const double lmv = taup / av;
+        const double emv = exp(-lmv);
+        double ab = 0.0, a0 = 0.0, a1t = 0.0;
+        if (beam) {
+          const double fac = (m == 0 ? 1.0 : 2.0) * fb / (4.0 * kPi);
+          ab = fma(fac * x0, exp(-A.tauc[(size_t)lc * A.ns + sl] * rmu0), scs);
+          const double e0l = rl(oE0, tt);
+          lay += upv ? ab * (1.0 - e0l * emv) / fma(av, rmu0, 1.0)
+                     : ab * dexp(e0l, emv, fma(-av, rmu0, 1.0), lmv);
+        }
+        if (therm) {
+          const double* q = qt[tt];
+          double ssa = A.nprop > 1 ? q[1] : 0.0;
+          if (ssa == 1.0) ssa = 1.0 - kDither;
+          const double f = ft[tt];
+          const double om = ssa * (1.0 - f) / (1.0 - ssa * f);
+          const double bt = rl(oBt, tt), slope = rl(oSl, tt);
+          const double ce0 = (1.0 - om) + 2.0 * we;
+          a1t = slope * ce0;
+          a0 = fma(bt, ce0, 2.0 * slope * wo);
+          lay += upv ? (a0 + a1t * mv) - (a0 + a1t * taup + a1t * mv) * emv
+                     : (a0 + a1t * taup + a1t * mv) - (a0 + a1t * mv) * emv;
+        }
+        if (iv < A.numu && v < A.nu) A.rsw[((size_t)lc * NE1 + iv) * nu + v] = lay;
+        double* ap = aux + lane * 4;
+        ap[0] = ab;
+        ap[1] = a0;
+        ap[2] = a1t;
+      }
+      lds_fence();
+      // ---- user depths inside the layer: the partial integral from the depth to the
+      // ray's entry (the scan adds the entry value's attenuated share) ----
+      {
+        const double ttop = A.taus[(size_t)lc * A.ns + sl];
+        const double tbot = A.taus[(size_t)(lc + 1) * A.ns + sl];
+        const double tau = tbot - ttop;
+        const double scale = tau > 0.0 ? taup / tau : 0.0;
+        // candidates: the caller's depths, or the layer's two levels -- whose scaled
+        // depth (tbot - ttop) tau'/tau can miss tau' by an ulp, and the scan then
+        // takes the interior branch for them as hd_rad_user_kernel does
+        const int k0 = A.utau ? 0 : lc, k1 = A.utau ? A.ntau : lc + 2;
+        for (int k = k0; k < k1; ++k) {
+          const double tu = user_tau(A, k, sl);
+          if (tu < ttop || tu > tbot) continue;  // uniform
+          const double tl = fmin(fmax((tu - ttop) * scale, 0.0), taup);
+          // the depth's layer along this ray: hd_rad_team_user_scan_kernel's walk
+          const bool mine = up ? (tu >= ttop && (lc == L - 1 || tu < tbot))
+                               : (tu <= tbot && (lc == 0 || tu > ttop));
+          const double tin = up ? taup : 0.0;
+          const bool need = aok && mine && tl != tin && tl != taup - tin;
+          if (!__any(need)) continue;  // uniform
+          double r = 0.0;
+          if (need) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              r += seg_exp(amp[q], fam ? -kq[q] : kq[q], tl, tin, fam ? taup : 0.0, muu);
+          }
+          red2[a * 8 + h * 2 + fam] = r;
+          lds_fence();
+          if (lane < 8 && ab0 + lane < A.numu && v < A.nu) {
+            const int iv = ab0 + lane;
+            const double mv = A.umu[iv];
+            const bool upv = mv > 0.0;
+            const bool minev = upv ? (tu >= ttop && (lc == L - 1 || tu < tbot))
+                                   : (tu <= tbot && (lc == 0 || tu > ttop));
+            const double tinv = upv ? taup : 0.0;
+            if (minev && tl != tinv && tl != taup - tinv) {
+              double rs = 0.0;
+#pragma unroll
+              for (int k2 = 0; k2 < 8; ++k2) rs += red2[lane * 8 + k2];
+              const double* ap = aux + lane * 4;
+              if (beam) rs += seg_exp(ap[0], rmu0, tl, tinv, 0.0, mv);
+              if (therm) {
+                const double e2 = exp(-(tinv - tl) / mv);
+                rs += (ap[1] + ap[2] * tl + ap[2] * mv) - (ap[1] + ap[2] * tinv + ap[2] * mv) * e2;
+              }
+              A.radm[((size_t)k * A.numu + iv) * nu + v] = rs;
+            }
+          }
+          lds_fence();
+        }
+      }
+    });
+  }
+}
+
+template <int NN>
+__global__ __launch_bounds__(256) void hd_rad_team_user_scan_kernel(RadArgs A) {
+  constexpr int nsym = NN * (NN + 1) / 2;
+  constexpr int NE1 = rad_layer_record_doubles(NN);
+  constexpr int NR = rad_rec_doubles(NN);
+  constexpr int oTp = nsym + NN * NN + 4 * NN + 2;
+  const Quad<NN>& Qc = tquad<NN>(c_qt);
+  const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t nu = A.nu;
+  if (id >= (long)nu * A.numu) return;
+  const int iu = (int)(id / (long)nu);
+  const int u = (int)(id - (long)iu * (long)nu);  // unit fastest: coalesced records
+  const int m = u / A.ns;
+  const int sl = u - m * A.ns;
+  const long s = A.s0 + sl;
+  const int L = A.nlyr;
+  const double muu = A.umu[iu];
+  const bool up = muu > 0.0;
+  const double anu = fabs(muu);
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
+  const double fb = A.fbeam ? A.fbeam[s] : 0.0;
+  const bool beam = fb > 0.0 && mu0 > 0.0;
+  const double rmu0 = beam ? 1.0 / mu0 : 0.0;
+  double cur = 0.0;
+  if (m == 0) {
+    if (up) {
+      const double* lv = A.lev + (size_t)L * 2 * NN * nu + u;
+      double fdn = 0.0;
+      for (int i = 0; i < NN; ++i) fdn = fma(Qc.g[i] * Qc.g[i], lv[(NN + i) * nu], fdn);
+      fdn *= 2.0 * kPi;
+      const double alb = A.albedo ? A.albedo[s] : 0.0;
+      if (beam) {
+        const double tb = A.tauc[(size_t)(L - 1) * A.ns + sl] +
+                          A.rrd[((size_t)(L - 1) * NR + oTp) * nu + u];
+        fdn += fb * mu0 * exp(-tb * rmu0);
+      }
+      cur = alb / kPi * fdn + (A.planck ? (1.0 - alb) * A.planckv[(size_t)(L + 1) * A.ns + sl]
+                                        : 0.0);
+    } else {
+      cur = A.fisot ? A.fisot[s] : 0.0;
+      if (A.planck) cur += A.planckv[(size_t)(L + 2) * A.ns + sl];
+    }
+  }
+  int k = up ? A.ntau - 1 : 0;
+  double chk = 0.0;
+  for (int step = 0; step < L; ++step) {
+    const int lc = up ? L - 1 - step : step;
+    const double ttop = A.taus[(size_t)lc * A.ns + sl];
+    const double tbot = A.taus[(size_t)(lc + 1) * A.ns + sl];
+    const double taup = A.rrd[((size_t)lc * NR + oTp) * nu + u];
+    const double emu = exp(-(taup / anu));
+    const double lay = A.rsw[((size_t)lc * NE1 + iu) * nu + u];
+    const double cin = cur;
+    const double cout = fma(cin, emu, lay);
+    const double tau = tbot - ttop;
+    const double scale = tau > 0.0 ? taup / tau : 0.0;
+    const double tin = up ? taup : 0.0;
+    auto put = [&](int kk) {
+      const double t = fmin(fmax((user_tau(A, kk, sl) - ttop) * scale, 0.0), taup);
+      double* o = A.radm + ((size_t)kk * A.numu + iu) * nu + u;
+      const double val = t == tin ? cin
+                       : t == taup - tin ? cout
+                       : fma(cin, exp(-fabs(tin - t) / anu), *o);  // *o: the partial integral
+      *o = val;
+      chk += val;
+    };
+    if (up) {
+      while (k >= 0 && user_tau(A, k, sl) >= ttop) put(k--);
+    } else {
+      while (k < A.ntau && user_tau(A, k, sl) <= tbot) put(k++);
+    }
+    cur = cout;
+  }
+  for (; k < A.ntau && !up; ++k) A.radm[((size_t)k * A.numu + iu) * nu + u] = cur;
+  if (!isfinite(chk)) {
+    atomicOr(&A.status[s], kStNonFinite);
+    atomicOr(A.anyerr, 1);
+  }
+}
+
+template <int NN>
+static hipError_t launch_rad_user(const RadArgs& a, hipStream_t stream) {
+  const unsigned nb = (unsigned)(((a.nu + 3) / 4) * (long)a.nlyr);
+  hipLaunchKernelGGL(hd_rad_team_user_kernel<NN>, dim3(nb), dim3(64), 0, stream, a);
+  const long nr = (long)a.nu * a.numu;
+  hipLaunchKernelGGL(hd_rad_team_user_scan_kernel<NN>, dim3((unsigned)((nr + 255) / 256)),
+                     dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_rad_team_user(int nn, const RadArgs& a, hipStream_t stream) {
+  if (a.numu > rad_layer_record_doubles(nn)) return hipErrorInvalidValue;
+  switch (nn) {
+    case 9: return launch_rad_user<9>(a, stream);
+    case 10: return launch_rad_user<10>(a, stream);
+    case 11: return launch_rad_user<11>(a, stream);
+    case 12: return launch_rad_user<12>(a, stream);
+    case 13: return launch_rad_user<13>(a, stream);
+    case 14: return launch_rad_user<14>(a, stream);
+    case 15: return launch_rad_user<15>(a, stream);
+    case 16: return launch_rad_user<16>(a, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
 
 template <int NN>
 static hipError_t launch_rad_sweep(const RadArgs& a, hipStream_t stream) {

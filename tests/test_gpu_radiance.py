@@ -131,7 +131,8 @@ def test_radiances_vs_oracle(nstr, planck):
 
 
 @pytest.mark.parametrize("numu", [8, 9, 16])
-@pytest.mark.parametrize("nstr,planck", [(4, False), (16, False), (16, True)])
+@pytest.mark.parametrize("nstr,planck", [(4, False), (16, False), (16, True), (24, False),
+                                         (32, True)])
 def test_radiances_many_angles_vs_oracle(numu, nstr, planck):
     """bench-like angle counts (numu 8 = the bench's, 9 = down/up unbalanced, 16);
     ncol*nwave*numu not a multiple of the 64-lane block, so the last block is partial"""
@@ -339,3 +340,49 @@ def test_radiance_umu0_as_given():
     bc0 = dict(bc, umu0=np.array([[0.5, 0.0, 0.5, 0.5]]))
     with pytest.raises(RuntimeError):
         d.forward(torch.as_tensor(prop, device=DEV), _dev(bc0))
+
+
+_USER_CHILD = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + '/tests')
+from test_gpu_radiance import _user_case
+np.save(sys.argv[5], _user_case(int(sys.argv[2]), sys.argv[3] == '1', sys.argv[4] == '1'))
+"""
+
+
+def _user_case(nstr, planck, usrtau):
+    rng = np.random.default_rng(3100 + nstr + 10 * planck + 20 * usrtau)
+    nwave, ncol, nlyr = 2, 5, 9
+    prop, bc, kw = _random_case(rng, nwave, ncol, nlyr, nstr, planck)
+    total = prop[..., 0].sum(axis=-1).min()
+    utau = np.sort(np.concatenate([[0.0, total], rng.uniform(0, total, 4)])) if usrtau else None
+    umu = [-1.0, -0.7, -0.31, -0.12, 0.1, 0.37, 0.66, 0.93, 1.0]
+    d = _disort(nstr, nlyr, nwave, ncol, flags="lamber,quiet,usrang" + (",usrtau" if usrtau else ""),
+                umu=umu, phi=[0.0, 90.0], utau=utau, planck=planck, wl=kw.get("wave_lower"),
+                wu=kw.get("wave_upper"))
+    t = None if "temf" not in kw else torch.as_tensor(kw["temf"], device=DEV)
+    d.forward(torch.as_tensor(prop, device=DEV), _dev(bc), t)
+    return d.get_rad().cpu().numpy()
+
+
+@pytest.mark.parametrize("nstr,planck,usrtau", [(20, False, False), (32, True, False),
+                                                (24, True, True), (32, False, True)])
+def test_team_user_kernel_matches_rolled(nstr, planck, usrtau, tmp_path):
+    """nstr 18..32 user angles: the team/MFMA kernel pair (per-(unit, layer) maps on
+    the matrix core + per-ray scan) against the one-lane-per-(unit, angle) kernel
+    (HD_RAD_USER=rolled, in a child process): the same integrals in another order,
+    to rounding -- levels only (the scaled level depths that miss tau' by an ulp
+    take the interior branch) and caller depths inside layers, nine angles (two
+    angle blocks)."""
+    import os
+    import subprocess
+    import sys
+    here = _user_case(nstr, planck, usrtau)
+    out = tmp_path / "rolled.npy"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, HD_RAD_USER="rolled")
+    subprocess.run([sys.executable, "-c", _USER_CHILD, root, str(nstr), "1" if planck else "0",
+                    "1" if usrtau else "0", str(out)], check=True, env=env, timeout=300)
+    other = np.load(out)
+    assert np.all(np.isfinite(here))
+    assert margin(_col_err(here, other)) < 1e-10, _col_err(here, other)
