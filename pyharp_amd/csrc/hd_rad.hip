@@ -1540,17 +1540,24 @@ static void launch_rad(const RadArgs& a, bool radiances, hipStream_t st) {
   else
     hipLaunchKernelGGL(hd_rad_sweep_kernel<NN>, dim3((unsigned)((a.nu + 63) / 64)), dim3(64), 0,
                        st, a);
-  const long nc = (long)a.nu * a.nlyr;
-  hipLaunchKernelGGL(hd_rad_const_kernel<NN>, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0,
-                     st, a);
+  const bool rad = radiances && a.numu > 0 && a.nphi > 0;
+  // nstr 18..32 with radiances: the team user-angle kernel also forms the layers'
+  // homogeneous constants (hd_team_mfma.hip), so the const kernel does not run
+  const bool team_user =
+      NN > kMaxRegNN && rad && a.numu <= rad_layer_record_doubles(NN) && !rad_user_rolled();
+  if (team_user) {
+    (void)hd::launch_rad_team_user(NN, a, st);
+  } else {
+    const long nc = (long)a.nu * a.nlyr;
+    hipLaunchKernelGGL(hd_rad_const_kernel<NN>, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0,
+                       st, a);
+  }
   const long nf = (long)a.ns * a.ntau;
   hipLaunchKernelGGL(hd_rad_flux_kernel<NN>, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, st,
                      a);
-  if (radiances && a.numu > 0 && a.nphi > 0) {
+  if (rad) {
     const long nr = (long)a.ns * a.numu;
-    if (NN > kMaxRegNN && a.numu <= rad_layer_record_doubles(NN) && !rad_user_rolled())
-      (void)hd::launch_rad_team_user(NN, a, st);  // team layout + MFMA (hd_team_mfma.hip)
-    else
+    if (!team_user)
       hipLaunchKernelGGL(hd_rad_user_kernel<NN>, dim3((unsigned)((nr + 63) / 64), (unsigned)a.nm),
                          dim3(64), 0, st, a);
     const long na = (long)a.ns * a.nphi * a.ntau * a.numu;

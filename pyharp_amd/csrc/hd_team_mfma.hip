@@ -1969,6 +1969,9 @@ __global__ __launch_bounds__(64, 2) void hd_rad_team_user_kernel(RadArgs A) {
     sfor<0, 4>([&](auto TT) {
       constexpr int tt = HD_K(TT);
       asm volatile("" : "+s"(uml[tt]));  // this problem's loads stay in its phase
+      int h_ = h, c_ = c;                 // as do its LDS reads and lane constants
+      asm volatile("" : "+v"(h_), "+v"(c_));
+      const int h = h_, c = c_;
       const int v = grp * 4 + tt;  // this problem's unit (>= nu: a repeat, not stored)
       const int m = mt[tt];
       const int sl = um[tt] - m * A.ns;
@@ -1979,6 +1982,78 @@ __global__ __launch_bounds__(64, 2) void hd_rad_team_user_kernel(RadArgs A) {
       const double rmu0 = beam ? 1.0 / mu0 : 0.0;
       const bool therm = A.planck && m == 0;
       const double taup = taupt[tt];
+      // ---- P^T = diag(sd) L V and Q^T = -diag(sd) L^-T V K, this problem's M layout
+      // (the A^T operand of the next product) ----
+      double PT[4], QT[4], cpl[4], cmi[4];
+      {
+        double vm[4], x[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = h + 4 * q;
+          const bool in = r < NN && c < NN;
+          vm[q] = in ? rl(oV + (in ? r * NN + c : 0), tt) : 0.0;
+        }
+        d4 p = {0.0, 0.0, 0.0, 0.0}, gq = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q] = S1[tt * kTile + c * kS + h + 4 * q];  // L^T (M)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) p = __builtin_amdgcn_mfma_f64_16x16x4f64(x[s4], vm[s4], p, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q] = S0[tt * kTile + c * kS + h + 4 * q];  // L^-1 (M)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) gq = __builtin_amdgcn_mfma_f64_16x16x4f64(x[s4], vm[s4], gq, 0, 0, 0);
+        // ---- the layer's homogeneous constants from its level intensities
+        // (hd_rad_const_kernel): C+ = (X^-1 s_top + Y^-1 d_top)/2, C- = (X^-1 s_bot -
+        // Y^-1 d_bot)/2 with X^-1 = (L^-T V)^T diag(g), Y^-1 = -K^-1 (L V)^T diag(g):
+        // one more product, B's columns 0/1 = g(s_top / s_bot) against L^-T V and
+        // 2/3 = g(d_top / d_bot) against L V ----
+        {
+          const int side = c & 1;
+          const double tsd = side ? taup : 0.0;
+          const double ebs = exp(-tsd * rmu0);
+          const double bt = rl(oBt, tt), slope = rl(oSl, tt);
+          const double b2 = 2.0 * fma(slope, tsd, bt);
+          const double* lv = A.lev + (size_t)(lc + side) * 2 * NN * nu + uml[tt];
+          double bx[4], by[4];
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) {
+            const int r = h + 4 * s4;
+            const bool in = r < NN && c < 4;
+            const int rr_ = in ? r : 0;
+            const double ipl = in ? lv[(size_t)rr_ * nu] : 0.0;
+            const double imi = in ? lv[(size_t)(NN + rr_) * nu] : 0.0;
+            const double zp = in ? rl(oZp + rr_, tt) : 0.0, zm = in ? rl(oZm + rr_, tt) : 0.0;
+            const double hr = in ? rl(oH + rr_, tt) : 0.0;
+            const double gr = Qc.g[rr_];
+            bx[s4] = (in && c < 2) ? gr * (ipl + imi - (zp + zm) * ebs - b2) : 0.0;
+            by[s4] = (in && c >= 2) ? gr * (ipl - imi - (zp - zm) * ebs - 2.0 * slope * hr) : 0.0;
+          }
+          d4 cacc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) cacc = __builtin_amdgcn_mfma_f64_16x16x4f64(gq[s4], bx[s4], cacc, 0, 0, 0);
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) cacc = __builtin_amdgcn_mfma_f64_16x16x4f64(p[s4], by[s4], cacc, 0, 0, 0);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int j = h + 4 * q;
+            const double kj = j < NN ? rl(oK + (j < NN ? j : 0), tt) : 0.0;
+            const double at_ = bc<0>(cacc[q]), ab_ = bc<1>(cacc[q]);
+            const double bt_ = bc<2>(cacc[q]), bb_ = bc<3>(cacc[q]);
+            cpl[q] = 0.5 * (at_ + (kj > 0.0 ? -bt_ / kj : 0.0));
+            cmi[q] = 0.5 * (ab_ - (kj > 0.0 ? -bb_ / kj : 0.0));
+            if (ab0 == 0 && v < A.nu && j < NN && c < 2)
+              A.cst[((size_t)lc * 2 * NN + c * NN + j) * nu + v] = c ? cmi[q] : cpl[q];
+          }
+        }
+        const double kc = c < NN ? rl(oK + (c < NN ? c : 0), tt) : 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = h + 4 * q;
+          const double sdr = r < NN ? Qc.sd[r < NN ? r : 0] : 0.0;
+          PT[q] = p[q] * sdr;
+          QT[q] = gq[q] * (-kc * sdr);
+        }
+      }
       // ---- this lane's rows of the angle's c_e (c < 8) or c_o (c >= 8) column, and
       // its share of x0 = sum_l g_l Y_l^m(mu) Y_l^m(-mu0) ----
       double cu[4] = {0.0, 0.0, 0.0, 0.0};
@@ -2025,35 +2100,6 @@ __global__ __launch_bounds__(64, 2) void hd_rad_team_user_kernel(RadArgs A) {
           xp = fma((l2 & 3) == h ? gl * yv : 0.0, y0s, xp);
         }
       }
-      // ---- P^T = diag(sd) L V and Q^T = -diag(sd) L^-T V K, this problem's M layout
-      // (the A^T operand of the next product) ----
-      double PT[4], QT[4];
-      {
-        double vm[4], x[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int r = h + 4 * q;
-          const bool in = r < NN && c < NN;
-          vm[q] = in ? rl(oV + (in ? r * NN + c : 0), tt) : 0.0;
-        }
-        d4 p = {0.0, 0.0, 0.0, 0.0}, g = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) x[q] = S1[tt * kTile + c * kS + h + 4 * q];  // L^T (M)
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) p = __builtin_amdgcn_mfma_f64_16x16x4f64(x[s4], vm[s4], p, 0, 0, 0);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) x[q] = S0[tt * kTile + c * kS + h + 4 * q];  // L^-1 (M)
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) g = __builtin_amdgcn_mfma_f64_16x16x4f64(x[s4], vm[s4], g, 0, 0, 0);
-        const double kc = c < NN ? rl(oK + (c < NN ? c : 0), tt) : 0.0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int r = h + 4 * q;
-          const double sdr = r < NN ? Qc.sd[r < NN ? r : 0] : 0.0;
-          PT[q] = p[q] * sdr;
-          QT[q] = g[q] * (-kc * sdr);
-        }
-      }
       // ---- [ce | cx] = [P | Q] . blockdiag(C_e, C_o) on the matrix core ----
       d4 hacc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -2076,7 +2122,7 @@ __global__ __launch_bounds__(64, 2) void hd_rad_team_user_kernel(RadArgs A) {
         const double own = hacc[q];
         const double oth = xperm<8>(own);
         const double ce = fam ? oth : own, cx = fam ? own : oth;
-        const double cc = jok ? A.cst[((size_t)lc * 2 * NN + fam * NN + jj) * nu + uml[tt]] : 0.0;
+        const double cc = jok ? (fam ? cmi[q] : cpl[q]) : 0.0;
         const double am = cc * (fam ? ce - cx : ce + cx);  // hpl_j (c < 8), hmi_j (c >= 8)
         const double kj = jok ? rl(oK + jj, tt) : 0.0;
         const double ek = jok ? rl(oEk + jj, tt) : 1.0;

@@ -14,7 +14,9 @@ for n in 32 24; do
   timeout -k 10 300 python scripts/bench_rad.py --nstr $n --steps 3 --warmup 1 > $OUT/rad_n${n}_team.json
   cat $OUT/rad_n${n}_team.json
 done
-HD_RAD_USER=rolled timeout -k 10 300 python scripts/bench_rad.py --nstr 32 --steps 2 --warmup 1 > $OUT/rad_n32_rolled.json
-cat $OUT/rad_n32_rolled.json
+timeout -k 10 300 python scripts/bench_rad.py --nstr 16 --steps 5 --warmup 2 > $OUT/rad_n16.json
+cat $OUT/rad_n16.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/stats_n32 -o kt --output-format csv -- python3 scripts/bench_rad.py --nstr 32 --steps 2 --warmup 1 > $OUT/stats_n32.json
 cut -d, -f1-5 $(ls $OUT/stats_n32/kt_kernel_stats.csv $OUT/stats_n32/*/kt_kernel_stats.csv 2>/dev/null | head -1) | head -12
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/stats_n16 -o kt --output-format csv -- python3 scripts/bench_rad.py --nstr 16 --steps 3 --warmup 1 > $OUT/stats_n16.json
+cut -d, -f1-5 $(ls $OUT/stats_n16/kt_kernel_stats.csv $OUT/stats_n16/*/kt_kernel_stats.csv 2>/dev/null | head -1) | head -12
