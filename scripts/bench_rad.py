@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--ntau", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--chunk", type=int, default=0, help="solves per chunk (0: by scratch budget)")
     a = ap.parse_args()
     from pyharp_amd import Disort, DisortOptions
     dev = torch.device("cuda", 0)
@@ -55,6 +56,9 @@ def main():
     op.user_mu(umu).user_phi(phi).user_tau(utau)
     op.ds().nlyr, op.ds().nstr, op.ds().nmom = L, n, n
     d = Disort(op)
+    if a.chunk:
+        from pyharp_amd.disort import _context
+        _context(0).set_chunk(a.chunk)
     p = torch.as_tensor(prop, device=dev)
     b = {k: torch.as_tensor(v, device=dev) for k, v in bc.items()}
     for _ in range(a.warmup):
@@ -78,7 +82,7 @@ def main():
         err = max(err, np.abs(uu[w, c] - ur[0, 0]).max() / np.abs(ur).max())
     print(json.dumps({"metric": "radiance solves/s (all azimuthal modes)",
                       "value": G * C / dt, "unit": "solves/s", "ms_per_step": dt * 1e3,
-                      "config": {"ncol": C, "ngpoint": G, "nstr": n, "nlyr": L, "numu": a.numu,
+                      "chunk": a.chunk or "auto", "config": {"ncol": C, "ngpoint": G, "nstr": n, "nlyr": L, "numu": a.numu,
                                  "nphi": a.nphi, "ntau": len(utau)},
                       "max_rel_err_subsample": err}))
 
