@@ -346,13 +346,14 @@ _USER_CHILD = r"""
 import sys, numpy as np
 sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + '/tests')
 from test_gpu_radiance import _user_case
-np.save(sys.argv[5], _user_case(int(sys.argv[2]), sys.argv[3] == '1', sys.argv[4] == '1'))
+np.save(sys.argv[5], _user_case(int(sys.argv[2]), sys.argv[3] == '1', sys.argv[4] == '1',
+                                int(sys.argv[6])))
 """
 
 
-def _user_case(nstr, planck, usrtau):
+def _user_case(nstr, planck, usrtau, nwave=2):
     rng = np.random.default_rng(3100 + nstr + 10 * planck + 20 * usrtau)
-    nwave, ncol, nlyr = 2, 5, 9
+    ncol, nlyr = 5, 9
     prop, bc, kw = _random_case(rng, nwave, ncol, nlyr, nstr, planck)
     total = prop[..., 0].sum(axis=-1).min()
     utau = np.sort(np.concatenate([[0.0, total], rng.uniform(0, total, 4)])) if usrtau else None
@@ -365,24 +366,27 @@ def _user_case(nstr, planck, usrtau):
     return d.get_rad().cpu().numpy()
 
 
-@pytest.mark.parametrize("nstr,planck,usrtau", [(20, False, False), (32, True, False),
-                                                (24, True, True), (32, False, True)])
-def test_team_user_kernel_matches_rolled(nstr, planck, usrtau, tmp_path):
+@pytest.mark.parametrize("nstr,planck,usrtau,nwave", [(20, False, False, 2), (32, True, False, 2),
+                                                      (24, True, True, 2), (32, False, True, 2),
+                                                      (18, True, True, 1)])
+def test_team_user_kernel_matches_rolled(nstr, planck, usrtau, nwave, tmp_path):
     """nstr 18..32 user angles: the team/MFMA kernel pair (per-(unit, layer) maps on
     the matrix core + per-ray scan) against the one-lane-per-(unit, angle) kernel
     (HD_RAD_USER=rolled, in a child process): the same integrals in another order,
     to rounding -- levels only (the scaled level depths that miss tau' by an ulp
     take the interior branch) and caller depths inside layers, nine angles (two
-    angle blocks)."""
+    angle blocks); 5 solves x 18 modes = 90 units leaves the last wave's group of
+    four units half empty."""
     import os
     import subprocess
     import sys
-    here = _user_case(nstr, planck, usrtau)
+    here = _user_case(nstr, planck, usrtau, nwave)
     out = tmp_path / "rolled.npy"
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, HD_RAD_USER="rolled")
     subprocess.run([sys.executable, "-c", _USER_CHILD, root, str(nstr), "1" if planck else "0",
-                    "1" if usrtau else "0", str(out)], check=True, env=env, timeout=300)
+                    "1" if usrtau else "0", str(out), str(nwave)], check=True, env=env,
+                   timeout=300)
     other = np.load(out)
     assert np.all(np.isfinite(here))
     assert margin(_col_err(here, other)) < 1e-10, _col_err(here, other)
