@@ -48,6 +48,17 @@ constexpr int kLayersPerBlockR = kLayerBlockR / 64;
 #ifndef HD_RUNROLL
 #define HD_RUNROLL _Pragma("unroll")
 #endif
+// rrd addressing in the const / flux / user kernels: [layer][element][unit] (unit
+// fastest: the one-lane kernels' coalesced layout) at nstr <= 16; at nstr 18..32 the
+// team kernels (hd_team_mfma.hip) write and read it, and it is [layer][unit][element]
+// (a team's accesses to one unit's record share lines)
+#ifdef HD_RAD_WIDE
+#define HD_RREC(lc, u) (A.rrd + ((size_t)(lc) * nu + (u)) * rad_rec_doubles(NN))
+#define HD_RS ((size_t)1)
+#else
+#define HD_RREC(lc, u) (A.rrd + (size_t)(lc) * rad_rec_doubles(NN) * nu + (u))
+#define HD_RS nu
+#endif
 
 template <int NN>
 struct RadTab {
@@ -848,20 +859,20 @@ __device__ __forceinline__ void load_layer(const RadArgs& A, int lc, int u, doub
                                            double (&kk)[NN]) {
   constexpr int nsym = NN * (NN + 1) / 2;
   const size_t nu = A.nu;
-  const double* rr = A.rrd + (size_t)lc * rad_rec_doubles(NN) * nu + u;
+  const double* rr = HD_RREC(lc, u);
   int e = 0;
 HD_RUNROLL
   for (int i = 0; i < NN; ++i)
 HD_RUNROLL
-    for (int k = 0; k <= i; ++k) lch[i][k] = rr[(e++) * nu];
+    for (int k = 0; k <= i; ++k) lch[i][k] = rr[(e++) * HD_RS];
 HD_RUNROLL
   for (int i = 0; i < NN; ++i) rd[i] = 1.0 / lch[i][i];
 HD_RUNROLL
   for (int i = 0; i < NN; ++i)
 HD_RUNROLL
-    for (int j = 0; j < NN; ++j) v[i][j] = rr[(nsym + i * NN + j) * nu];
+    for (int j = 0; j < NN; ++j) v[i][j] = rr[(nsym + i * NN + j) * HD_RS];
 HD_RUNROLL
-  for (int j = 0; j < NN; ++j) kk[j] = rr[(nsym + NN * NN + j) * nu];
+  for (int j = 0; j < NN; ++j) kk[j] = rr[(nsym + NN * NN + j) * HD_RS];
 }
 
 template <int NN>
@@ -879,8 +890,8 @@ __global__ __launch_bounds__(256) void hd_rad_const_kernel(RadArgs A) {
   constexpr int oZp = nsym + NN * NN + NN, oZm = oZp + NN, oH = oZm + NN, oBt = oH + NN;
   double lch[NN][NN], rd[NN], v[NN][NN], kk[NN];
   load_layer<NN>(A, lc, u, lch, rd, v, kk);
-  const double* rr = A.rrd + (size_t)lc * rad_rec_doubles(NN) * nu + u;
-  const double bt = rr[oBt * nu], slope = rr[(oBt + 1) * nu], taup = rr[(oBt + 2) * nu];
+  const double* rr = HD_RREC(lc, u);
+  const double bt = rr[oBt * HD_RS], slope = rr[(oBt + 1) * HD_RS], taup = rr[(oBt + 2) * HD_RS];
   const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
   const double fb = A.fbeam ? A.fbeam[s] : 0.0;
   const double rmu0 = (fb > 0.0 && mu0 > 0.0) ? 1.0 / mu0 : 0.0;
@@ -895,7 +906,7 @@ HD_RUNROLL
 HD_RUNROLL
     for (int i = 0; i < NN; ++i) {
       const double ipl = lv[i * nu], imi = lv[(NN + i) * nu];
-      const double zp = rr[(oZp + i) * nu], zm = rr[(oZm + i) * nu], h = rr[(oH + i) * nu];
+      const double zp = rr[(oZp + i) * HD_RS], zm = rr[(oZm + i) * HD_RS], h = rr[(oH + i) * HD_RS];
       xs[i] = Qc.g[i] * (ipl + imi - (zp + zm) * eb - b2);
       yd[i] = Qc.g[i] * (ipl - imi - (zp - zm) * eb - 2.0 * slope * h);
     }
@@ -952,8 +963,8 @@ __global__ __launch_bounds__(256) void hd_rad_flux_kernel(RadArgs A) {
   const double tau = A.taus[(size_t)(lc + 1) * A.ns + sl] - ttop;
   double lch[NN][NN], rd[NN], v[NN][NN], kk[NN];
   load_layer<NN>(A, lc, u, lch, rd, v, kk);
-  const double* rr = A.rrd + (size_t)lc * rad_rec_doubles(NN) * nu + u;
-  const double bt = rr[oBt * nu], slope = rr[(oBt + 1) * nu], taup = rr[(oBt + 2) * nu];
+  const double* rr = HD_RREC(lc, u);
+  const double bt = rr[oBt * HD_RS], slope = rr[(oBt + 1) * HD_RS], taup = rr[(oBt + 2) * HD_RS];
   const double scale = tau > 0.0 ? taup / tau : 0.0;
   const double t = fmin(fmax((tu - ttop) * scale, 0.0), taup);
   const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
@@ -994,7 +1005,7 @@ HD_RUNROLL
   double up = 0.0, dn = 0.0;
 HD_RUNROLL
   for (int i = 0; i < NN; ++i) {
-    const double zp = rr[(oZp + i) * nu], zm = rr[(oZm + i) * nu], h = rr[(oH + i) * nu];
+    const double zp = rr[(oZp + i) * HD_RS], zm = rr[(oZm + i) * HD_RS], h = rr[(oH + i) * HD_RS];
     const double ipl = 0.5 * (gs[i] - gd[i]) + Qc.g[i] * (zp * eb + bb + slope * h);
     const double imi = 0.5 * (gs[i] + gd[i]) + Qc.g[i] * (zm * eb + bb - slope * h);
     up = fma(Qc.g[i], ipl, up);
@@ -1058,7 +1069,7 @@ HD_RUNROLL
       const double alb = A.albedo ? A.albedo[s] : 0.0;
       if (beam) {
         const double tb = A.tauc[(size_t)(L - 1) * A.ns + sl] +
-                          A.rrd[((size_t)(L - 1) * rad_rec_doubles(NN) + oBt + 2) * nu + u];
+                          HD_RREC(L - 1, u)[(oBt + 2) * HD_RS];
         fdn += fb * mu0 * exp(-tb * rmu0);
       }
       cur = alb / kPi * fdn + (A.planck ? (1.0 - alb) * A.planckv[(size_t)(L + 1) * A.ns + sl]
@@ -1110,8 +1121,8 @@ HD_RUNROLL
     };
     if (m & 1) lsum(1);
     else lsum(0);
-    const double* rr = A.rrd + (size_t)lc * rad_rec_doubles(NN) * nu + u;
-    const double bt = rr[oBt * nu], slope = rr[(oBt + 1) * nu], taup = rr[(oBt + 2) * nu];
+    const double* rr = HD_RREC(lc, u);
+    const double bt = rr[oBt * HD_RS], slope = rr[(oBt + 1) * HD_RS], taup = rr[(oBt + 2) * HD_RS];
     // ce = V^T L^T (sd cue), co = -k V^T L^-1 (sd cuo); L and V streamed from the
     // record (each element used once), not held in registers
     double a1[NN], b1[NN];
@@ -1122,32 +1133,32 @@ HD_RUNROLL
     }
 HD_RUNROLL
     for (int i = 0; i < NN; ++i) {  // row i of L: a1 += L[i][:]^T (sd cue)_i ; b1 forward subst.
-      const double* li = rr + (size_t)(i * (i + 1) / 2) * nu;
+      const double* li = rr + (size_t)(i * (i + 1) / 2) * HD_RS;
       const double ce_i = Qc.sd[i] * cue[i];
       double t = b1[i];
 HD_RUNROLL
       for (int k2 = 0; k2 < i; ++k2) {
-        const double l = li[k2 * nu];
+        const double l = li[k2 * HD_RS];
         a1[k2] = fma(l, ce_i, a1[k2]);
         t = fma(-l, b1[k2], t);
       }
-      const double d = li[i * nu];
+      const double d = li[i * HD_RS];
       a1[i] = fma(d, ce_i, a1[i]);
       b1[i] = t / d;
     }
     const double* co = A.cst + (size_t)lc * 2 * NN * nu + u;
-    const double* vr = rr + (size_t)nsym * nu;
+    const double* vr = rr + (size_t)nsym * HD_RS;
     double kk[NN], hpl[NN], hmi[NN];
 HD_RUNROLL
     for (int j = 0; j < NN; ++j) {
       hpl[j] = hmi[j] = 0.0;
-      kk[j] = rr[(nsym + NN * NN + j) * nu];
+      kk[j] = rr[(nsym + NN * NN + j) * HD_RS];
     }
 HD_RUNROLL
     for (int i = 0; i < NN; ++i)
 HD_RUNROLL
       for (int j = 0; j < NN; ++j) {
-        const double vij = vr[(i * NN + j) * nu];
+        const double vij = vr[(i * NN + j) * HD_RS];
         hpl[j] = fma(vij, a1[i], hpl[j]);  // ce
         hmi[j] = fma(vij, b1[i], hmi[j]);  // V^T b1
       }
@@ -1162,7 +1173,7 @@ HD_RUNROLL
       double sc = 0.0;
 HD_RUNROLL
       for (int i = 0; i < NN; ++i) {
-        const double zp = rr[(oZp + i) * nu], zm = rr[(oZm + i) * nu];
+        const double zp = rr[(oZp + i) * HD_RS], zm = rr[(oZm + i) * HD_RS];
         sc = fma(Qc.w[i], fma(cue[i], zp + zm, cuo[i] * (zp - zm)), sc);
       }
       ab = fma(fac * x0, exp(-A.tauc[(size_t)lc * A.ns + sl] * rmu0), sc);
@@ -1172,7 +1183,7 @@ HD_RUNROLL
 HD_RUNROLL
       for (int i = 0; i < NN; ++i) {
         we = fma(Qc.w[i], cue[i], we);
-        wo = fma(Qc.w[i] * cuo[i], rr[(oH + i) * nu], wo);
+        wo = fma(Qc.w[i] * cuo[i], rr[(oH + i) * HD_RS], wo);
       }
       const double ce0 = (1.0 - om) + 2.0 * we;
       a1t = slope * ce0;
@@ -1203,13 +1214,13 @@ HD_RUNROLL
     double lay = 0.0;
 HD_RUNROLL
     for (int j = 0; j < NN; ++j) {
-      const double ek = rr[(oEk + j) * nu];
+      const double ek = rr[(oEk + j) * HD_RS];
       const double reg = (1.0 - ek * emu) / fma(kk[j], anu, 1.0);
       const double sng = dexp(ek, emu, fma(-kk[j], anu, 1.0), lmu);
       lay = up ? fma(hpl[j], reg, fma(hmi[j], sng, lay)) : fma(hpl[j], sng, fma(hmi[j], reg, lay));
     }
     if (beam) {
-      const double e0l = rr[oE0 * nu];
+      const double e0l = rr[oE0 * HD_RS];
       lay += up ? ab * (1.0 - e0l * emu) / fma(anu, rmu0, 1.0)
                 : ab * dexp(e0l, emu, fma(-anu, rmu0, 1.0), lmu);
     }

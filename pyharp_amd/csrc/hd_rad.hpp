@@ -46,9 +46,10 @@ struct RadArgs {
   const double* phi;   // [nphi] degrees
   const double* utau;  // [ntau] unscaled, ascending; null = the nlyr+1 levels
   // scratch (unit u = m*ns + sl is the fastest index)
-  double* rsw;   // [nlyr][ne1][nu]   layer operators (flux-kernel layout)
-  double* rrd;   // [nlyr][rad_rec][nu]
-  double* bsub;  // [nlyr][rad_bsub][nu]
+  double* rsw;   // [nlyr][ne1][nu]   layer operators (flux-kernel layout); nstr > 16:
+                 //   [nlyr][nu][ne1] (team kernels, unit-contiguous)
+  double* rrd;   // [nlyr][rad_rec][nu]; nstr > 16: [nlyr][nu][rad_rec]
+  double* bsub;  // [nlyr][rad_bsub][nu]; nstr > 16: [nlyr][nu][rad_bsub]
   double* lev;   // [nlyr+1][2NN][nu]   I+ (NN) then I- (NN) per level, solver order
   double* cst;   // [nlyr][2NN][nu]     C+ then C-
   double* radm;  // [ntau*numu][nu]     radiance per mode

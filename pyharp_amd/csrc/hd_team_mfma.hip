@@ -1143,9 +1143,10 @@ __global__ __launch_bounds__(64, 2) void hd_team_mfma_sweep_lean_kernel(SweepArg
 // at m = 0, plus L, V, k, the particular solution and the exponentials kept for
 // the radiance kernels) on the team layout with the dense products on the matrix
 // core: hd_team_mfma_layer_kernel's algebra, four units per wave.  Writes the
-// radiance kernels' unit-fastest records (rsw: R~/T~ packed upper, S~+-, tau';
-// rrd: L packed, V, k, Z+-, h, B_top, dB/dtau', tau', omega', e^{-k tau'},
-// e^{-tau'/mu0}) exactly as hd_rad_layer_kernel lays them out.
+// radiance records unit-contiguous ([layer][unit][element]): rsw (R~/T~ packed
+// upper, S~+-, tau') for the team sweep, rrd (L packed, V, k, Z+-, h, B_top,
+// dB/dtau', tau', omega', e^{-k tau'}, e^{-tau'/mu0}) for the team user-angle kernel
+// and the rolled flux / const / user kernels (hd_rad.hip's HD_RREC at these sizes).
 // ============================================================================
 template <int NN>
 __global__ __launch_bounds__(64, 1) void hd_rad_team_layer_kernel(RadArgs A) {
@@ -1184,8 +1185,8 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_layer_kernel(RadArgs A) {
   int um[4];
 #pragma unroll
   for (int tt = 0; tt < 4; ++tt) um[tt] = grp * 4 + tt < A.nu ? grp * 4 + tt : grp * 4;
-  double* rr = A.rrd + (size_t)lc * NR * nu + u;   // element e: rr[e * nu]
-  double* out = A.rsw + (size_t)lc * NE1 * nu;    // element e of unit v: out[e * nu + v]
+  double* rr = A.rrd + ((size_t)lc * nu + u) * NR;   // element e: rr[e]
+  double* out = A.rsw + (size_t)lc * NE1 * nu;    // element e of unit v: out[v * NE1 + e]
 
   for (int k = lane; k < 2 * kSet; k += 64) lds[k] = 0.0;
   lds_fence();
@@ -1271,7 +1272,7 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_layer_kernel(RadArgs A) {
   if (wr) {  // L, packed lower row-major: row i holds lch[k], k <= i
     sfor<0, NN>([&](auto K) {
       constexpr int k = HD_K(K);
-      if (k <= i) rr[(size_t)(i * (i + 1) / 2 + k) * nu] = lch[k];
+      if (k <= i) rr[i * (i + 1) / 2 + k] = lch[k];
     });
   }
 
@@ -1302,22 +1303,22 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_layer_kernel(RadArgs A) {
     cvec = sd_i * mu_i;
     team_lsolve<NN>(lch, rdl, cvec);
     team_usolve<NN>(lt, rdl, cvec);
-    if (wr) rr[(size_t)(oH + i) * nu] = rg_i * cvec;
+    if (wr) rr[oH + i] = rg_i * cvec;
     cvec = fma(b1 * rg_i, cvec, db) * msk;
     if (valid && i == 0) {
-      rr[(size_t)oBt * nu] = bt;
-      rr[(size_t)oSl * nu] = 0.5 * b1;
+      rr[oBt] = bt;
+      rr[oSl] = 0.5 * b1;
     }
   } else {
-    if (wr) rr[(size_t)(oH + i) * nu] = 0.0;
+    if (wr) rr[oH + i] = 0.0;
     if (valid && i == 0) {
-      rr[(size_t)oBt * nu] = 0.0;
-      rr[(size_t)oSl * nu] = 0.0;
+      rr[oBt] = 0.0;
+      rr[oSl] = 0.0;
     }
   }
   if (valid && i == 0) {
-    rr[(size_t)oTp * nu] = taup;
-    rr[(size_t)oOm * nu] = om;
+    rr[oTp] = taup;
+    rr[oOm] = om;
   }
   {
     double z[NN];
@@ -1359,8 +1360,8 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_layer_kernel(RadArgs A) {
     G[t * 32 + i] = sqrt(delta) * msk;
     G[t * 32 + 16 + i] = sqrt(kk * th) * msk;
     if (wr) {
-      rr[(size_t)(oK + i) * nu] = kk;
-      rr[(size_t)(oEk + i) * nu] = 1.0 - mm;  // exp(-k tau')
+      rr[oK + i] = kk;
+      rr[oEk + i] = 1.0 - mm;  // exp(-k tau')
     }
   }
 
@@ -1385,11 +1386,11 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_layer_kernel(RadArgs A) {
 #pragma unroll
       for (int tt = 0; tt < 4; ++tt) {
         const bool ok = grp * 4 + tt < A.nu;
-        double* rv = A.rrd + (size_t)lc * NR * nu + um[tt];
+        double* rv = A.rrd + ((size_t)lc * nu + um[tt]) * NR;
 #pragma unroll
         for (int q2 = 0; q2 < 4; ++q2) {
           const int r = h + 4 * q2;
-          if (ok && r < NN && c < NN) rv[(size_t)(oV + r * NN + c) * nu] = X[tt][q2];
+          if (ok && r < NN && c < NN) rv[oV + r * NN + c] = X[tt][q2];
         }
       }
     }
@@ -1419,10 +1420,10 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_layer_kernel(RadArgs A) {
       e0 = exp(-taup * rmu0);
     }
     if (wr) {
-      rr[(size_t)(oZp + i) * nu] = zp;
-      rr[(size_t)(oZm + i) * nu] = zm;
+      rr[oZp + i] = zp;
+      rr[oZm + i] = zm;
     }
-    if (valid && i == 0) rr[(size_t)oE0 * nu] = e0;
+    if (valid && i == 0) rr[oE0] = e0;
     get_m(S0, h, c, Y);            // W (M)
     mprod<false>(U, Y, X, h, c);   // U^T W
 #pragma unroll
@@ -1487,8 +1488,8 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_layer_kernel(RadArgs A) {
       const double trv = (Am[tt][q2] + Ap[tt][q2]) - (r == c ? 1.0 : 0.0);
       if (ok && r <= c && c < NN) {
         const int e = sym_index<NN>(r, c);
-        out[(size_t)e * nu + um[tt]] = rrv;
-        out[(size_t)(nsym + e) * nu + um[tt]] = trv;
+        out[(size_t)um[tt] * NE1 + e] = rrv;
+        out[(size_t)um[tt] * NE1 + nsym + e] = trv;
       }
       chk += rrv + trv;
     }
@@ -1502,11 +1503,11 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_layer_kernel(RadArgs A) {
   const double sp = g_i * (zp * (1.0 - e0) - db) + pv - qv;
   const double sm = g_i * (-zm * (1.0 - e0) + db) - pv - qv;
   if (wr) {
-    out[(size_t)(2 * nsym + i) * nu + u] = sp;
-    out[(size_t)(2 * nsym + NN + i) * nu + u] = sm;
+    out[(size_t)u * NE1 + 2 * nsym + i] = sp;
+    out[(size_t)u * NE1 + 2 * nsym + NN + i] = sm;
   }
   chk += sp + sm;
-  if (valid && i == 0) out[(size_t)(2 * nsym + 2 * NN) * nu + u] = taup;
+  if (valid && i == 0) out[(size_t)u * NE1 + 2 * nsym + 2 * NN] = taup;
   if (act && !isfinite(chk + taup)) st |= kStNonFinite;
   if (valid && st) {
     atomicOr(&A.status[s], st);
@@ -1519,9 +1520,11 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_layer_kernel(RadArgs A) {
 // back-substitution (hd_rad_sweep_kernel: the stack state R_above/S_down and
 // I+/I- kept at every level) on the team layout with the dense products on the
 // matrix core -- four units (solve, azimuthal mode) per wave, the arithmetic of
-// hd_team_mfma_sweep_kernel above.  Reads and writes the radiance kernels'
-// unit-fastest records ([element][unit]: rsw, bsub, lev) unchanged, so the
-// per-lane kernels around it (hd_rad_wide.hip) need nothing new.  Replaces a
+// hd_team_mfma_sweep_kernel above.  The layer-operator and back-substitution
+// records (rsw, bsub) are unit-contiguous at these sizes ([layer][unit][element]:
+// a team's loads and stores of one unit's record hit neighbouring lines, where the
+// unit-fastest layout the one-lane kernels use put every lane on its own line);
+// lev keeps the unit-fastest layout the per-lane kernels read.  Replaces a
 // one-lane-per-unit loop whose 16 x 16 matrices lived in private memory
 // (62% of the nstr-32 radiance time, profiles/r03/).
 // ============================================================================
@@ -1588,15 +1591,15 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_sweep_kernel(RadArgs A) {
   double tauc = 0.0;
 
   for (int lc = 0; lc < L; ++lc) {
-    const double* lp = A.rsw + (size_t)lc * NE1 * nu;  // element e of unit v: lp[e*nu + v]
+    const double* lp = A.rsw + (size_t)lc * NE1 * nu;  // element e of unit v: lp[v*NE1 + e]
     double* bp = A.bsub + (size_t)lc * NB * nu;
     // the stack above this layer: R_above (packed upper, row i from j = i) and S_down
     if (wr) {
       sfor<0, NN>([&](auto J) {
         constexpr int j = HD_K(J);
-        if (j >= i) bp[(size_t)(NN * NN + NN + sym_index<NN>(i, j)) * nu + u] = ra[j];
+        if (j >= i) bp[(size_t)u * NB + NN * NN + NN + sym_index<NN>(i, j)] = ra[j];
       });
-      bp[(size_t)(NN * NN + NN + nsym + i) * nu + u] = sd;
+      bp[(size_t)u * NB + NN * NN + NN + nsym + i] = sd;
     }
     // R~, T~ (packed upper) of the four units in M layout; this unit's rows (T layout)
     double rm[4][4], tm[4][4];
@@ -1607,17 +1610,17 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_sweep_kernel(RadArgs A) {
         const int r = h + 4 * q;
         const bool in = r < NN && c < NN;
         const int e = in ? sym_index<NN>(r, c) : 0;
-        rm[tt][q] = in ? lp[(size_t)e * nu + um[tt]] : 0.0;
-        tm[tt][q] = in ? lp[(size_t)(nsym + e) * nu + um[tt]] : 0.0;
+        rm[tt][q] = in ? lp[(size_t)um[tt] * NE1 + e] : 0.0;
+        tm[tt][q] = in ? lp[(size_t)um[tt] * NE1 + nsym + e] : 0.0;
       }
     double rl[NN], tr[NN];
     sfor<0, NN>([&](auto J) {
       const int e = sym_index<NN>(ii, HD_K(J));
-      rl[HD_K(J)] = lp[(size_t)e * nu + u] * msk;
-      tr[HD_K(J)] = lp[(size_t)(nsym + e) * nu + u] * msk;
+      rl[HD_K(J)] = lp[(size_t)u * NE1 + e] * msk;
+      tr[HD_K(J)] = lp[(size_t)u * NE1 + nsym + e] * msk;
     });
-    const double spl = lp[(size_t)(2 * nsym + ii) * nu + u] * msk;
-    const double sml = lp[(size_t)(2 * nsym + NN + ii) * nu + u] * msk;
+    const double spl = lp[(size_t)u * NE1 + 2 * nsym + ii] * msk;
+    const double sml = lp[(size_t)u * NE1 + 2 * nsym + NN + ii] * msk;
     // W1 = I - R A on the matrix core, to team rows through LDS
     {
       double pw[4][4];
@@ -1665,7 +1668,7 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_sweep_kernel(RadArgs A) {
     // u = A t1 + Sd
     double uv = sd;
     sfor<0, NN>([&](auto K) { uv = fma(ra[HD_K(K)], bc<HD_K(K)>(t1), uv); });
-    if (wr) bp[(size_t)(NN * NN + i) * nu + u] = t1;
+    if (wr) bp[(size_t)u * NB + NN * NN + i] = t1;
     // ZT = W1^-1 T = U^-1 (L^-1 T): columns of the triangular inverses on the team
     // (lane i: row i of the transposed inverse), the products on the matrix core
     {
@@ -1711,7 +1714,7 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_sweep_kernel(RadArgs A) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int r = h + 4 * q;
-          if (ok && r < NN && c < NN) bp[(size_t)(r * NN + c) * nu + um[tt]] = zm[tt][q];
+          if (ok && r < NN && c < NN) bp[(size_t)um[tt] * NB + r * NN + c] = zm[tt][q];
         }
       }
       mprod<false>(ram, zm, pm, h, c);  // A ZT
@@ -1726,7 +1729,7 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_sweep_kernel(RadArgs A) {
     }
     get_rows<NN>(S0, t, i, ra);
     sfor<0, NN>([&](auto J) { ra[HD_K(J)] *= msk; });
-    tauc += lp[(size_t)(2 * nsym + 2 * NN) * nu + u];
+    tauc += lp[(size_t)u * NE1 + 2 * nsym + 2 * NN];
   }
 
   // ---- Lambertian surface (mode 0): I+ = g x ----
@@ -1752,14 +1755,14 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_sweep_kernel(RadArgs A) {
   // ---- back-substitution bottom -> top, I+ and I- at every level ----
   for (int lc = L - 1; lc >= 0; --lc) {
     const double* bp = A.bsub + (size_t)lc * NB * nu;
-    double nip = bp[(size_t)(NN * NN + ii) * nu + u] * msk;
+    double nip = bp[(size_t)u * NB + NN * NN + ii] * msk;
     sfor<0, NN>([&](auto J) {
-      nip = fma(bp[(size_t)(ii * NN + HD_K(J)) * nu + u] * msk, bc<HD_K(J)>(ip), nip);
+      nip = fma(bp[(size_t)u * NB + ii * NN + HD_K(J)] * msk, bc<HD_K(J)>(ip), nip);
     });
     ip = nip;
-    double dn = bp[(size_t)(NN * NN + NN + nsym + ii) * nu + u] * msk;
+    double dn = bp[(size_t)u * NB + NN * NN + NN + nsym + ii] * msk;
     sfor<0, NN>([&](auto J) {
-      const double r = bp[(size_t)(NN * NN + NN + sym_index<NN>(ii, HD_K(J))) * nu + u] * msk;
+      const double r = bp[(size_t)u * NB + NN * NN + NN + sym_index<NN>(ii, HD_K(J))] * msk;
       dn = fma(r, bc<HD_K(J)>(ip), dn);
     });
     double* lv = A.lev + (size_t)lc * 2 * NN * nu;
@@ -1902,8 +1905,8 @@ __global__ __launch_bounds__(64, 2) void hd_rad_team_user_kernel(RadArgs A) {
   int um[4];
 #pragma unroll
   for (int tt = 0; tt < 4; ++tt) um[tt] = grp * 4 + tt < A.nu ? grp * 4 + tt : grp * 4;
-  const double* rec = A.rrd + (size_t)lc * NR * nu;  // element e of unit v: rec[e * nu + v]
-  auto rv = [&](int e, int tt) { return rec[(size_t)e * nu + um[tt]]; };
+  const double* rec = A.rrd + (size_t)lc * nu * NR;  // element e of unit v: rec[v * NR + e]
+  auto rv = [&](int e, int tt) { return rec[(size_t)um[tt] * NR + e]; };
 
   for (int k = lane; k < 2 * kSet; k += 64) lds[k] = 0.0;
   lds_fence();
@@ -1915,9 +1918,9 @@ __global__ __launch_bounds__(64, 2) void hd_rad_team_user_kernel(RadArgs A) {
     double lrow[NN];
     sfor<0, NN>([&](auto K) {
       constexpr int k = HD_K(K);
-      lrow[k] = (act && k <= ii) ? rec[(size_t)(r0 + (k <= ii ? k : 0)) * nu + u] : 0.0;
+      lrow[k] = (act && k <= ii) ? rec[(size_t)u * NR + r0 + (k <= ii ? k : 0)] : 0.0;
     });
-    double rdl = act ? 1.0 / rec[(size_t)(r0 + ii) * nu + u] : 0.0;
+    double rdl = act ? 1.0 / rec[(size_t)u * NR + r0 + ii] : 0.0;
     double z[NN];
     team_tri_inverse_col<NN>(lrow, rdl, z);  // row i of L^-T
     put_rows<NN>(S0, t, i, z);
@@ -1957,7 +1960,7 @@ __global__ __launch_bounds__(64, 2) void hd_rad_team_user_kernel(RadArgs A) {
       uml[tt] = um[tt];
       asm volatile("" : "+s"(uml[tt]));
     }
-    auto rl = [&](int e, int tt) { return rec[(size_t)e * nu + uml[tt]]; };
+    auto rl = [&](int e, int tt) { return rec[(size_t)uml[tt] * NR + e]; };
     const int iu = ab0 + a;
     const bool aok = iu < A.numu;
     const double muu = aok ? A.umu[iu] : 1.0;
@@ -2190,7 +2193,7 @@ __global__ __launch_bounds__(64, 2) void hd_rad_team_user_kernel(RadArgs A) {
           lay += upv ? (a0 + a1t * mv) - (a0 + a1t * taup + a1t * mv) * emv
                      : (a0 + a1t * taup + a1t * mv) - (a0 + a1t * mv) * emv;
         }
-        if (iv < A.numu && v < A.nu) A.rsw[((size_t)lc * NE1 + iv) * nu + v] = lay;
+        if (iv < A.numu && v < A.nu) A.rsw[((size_t)lc * nu + v) * NE1 + iv] = lay;
         double* ap = aux + lane * 4;
         ap[0] = ab;
         ap[1] = a0;
@@ -2286,7 +2289,7 @@ __global__ __launch_bounds__(256) void hd_rad_team_user_scan_kernel(RadArgs A) {
       const double alb = A.albedo ? A.albedo[s] : 0.0;
       if (beam) {
         const double tb = A.tauc[(size_t)(L - 1) * A.ns + sl] +
-                          A.rrd[((size_t)(L - 1) * NR + oTp) * nu + u];
+                          A.rrd[((size_t)(L - 1) * nu + u) * NR + oTp];
         fdn += fb * mu0 * exp(-tb * rmu0);
       }
       cur = alb / kPi * fdn + (A.planck ? (1.0 - alb) * A.planckv[(size_t)(L + 1) * A.ns + sl]
@@ -2302,9 +2305,9 @@ __global__ __launch_bounds__(256) void hd_rad_team_user_scan_kernel(RadArgs A) {
     const int lc = up ? L - 1 - step : step;
     const double ttop = A.taus[(size_t)lc * A.ns + sl];
     const double tbot = A.taus[(size_t)(lc + 1) * A.ns + sl];
-    const double taup = A.rrd[((size_t)lc * NR + oTp) * nu + u];
+    const double taup = A.rrd[((size_t)lc * nu + u) * NR + oTp];
     const double emu = exp(-(taup / anu));
-    const double lay = A.rsw[((size_t)lc * NE1 + iu) * nu + u];
+    const double lay = A.rsw[((size_t)lc * nu + u) * NE1 + iu];
     const double cin = cur;
     const double cout = fma(cin, emu, lay);
     const double tau = tbot - ttop;
