@@ -1274,6 +1274,7 @@ int rad_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in,
     a.nphi = nphi;
     a.ntau = ntau;
     a.corint = rad->corint != 0;
+    a.sink = ctx->sink;
     hipError_t e = hd::launch_rad_chunk(nn, a, radiances, stream);
     if (e != hipSuccess)
       return fail(ctx, HD_EHIP, "hd_solve_radiance: launch failed: %s", hipGetErrorString(e));

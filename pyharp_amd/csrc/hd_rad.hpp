@@ -70,6 +70,7 @@ struct RadArgs {
   int max_sweeps;
   int numu, nphi, ntau;
   int corint;  // Nakajima-Tanaka TMS correction of the single scattering
+  double* sink;  // team kernels: target of the stores a lane does not own (>= 64 doubles)
 };
 
 // int_{t1}^{t2} a exp(-c (t - tref)) exp(-(t - t1)/mu) dt/mu, t1 = evaluation

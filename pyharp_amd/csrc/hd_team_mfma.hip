@@ -1149,7 +1149,7 @@ __global__ __launch_bounds__(64, 2) void hd_team_mfma_sweep_lean_kernel(SweepArg
 // and the rolled flux / const / user kernels (hd_rad.hip's HD_RREC at these sizes).
 // ============================================================================
 template <int NN>
-__global__ __launch_bounds__(64, 1) void hd_rad_team_layer_kernel(RadArgs A) {
+__global__ __launch_bounds__(64, 2) void hd_rad_team_layer_kernel(RadArgs A) {
   __shared__ double lds[2 * kSet + 4 * 2 * 16];
   double* S0 = lds;
   double* S1 = lds + kSet;
@@ -1269,10 +1269,14 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_layer_kernel(RadArgs A) {
   // L L^T = S-
   double lt[NN], rdl;
   if (!team_chol<NN, true>(lch, lt, rdl)) st |= kStEigen;
-  if (wr) {  // L, packed lower row-major: row i holds lch[k], k <= i
+  {  // L, packed lower row-major: row i holds lch[k], k <= i.  Branch-free: the
+     // elements a lane does not own go to the sink.  Stores under a lane-dependent
+     // condition inside the unrolled loop cost 1 KB of spill at two waves per SIMD
+    double* lrow = rr + i * (i + 1) / 2;
     sfor<0, NN>([&](auto K) {
       constexpr int k = HD_K(K);
-      if (k <= i) rr[i * (i + 1) / 2 + k] = lch[k];
+      double* dst = (wr && k <= i) ? &lrow[k] : A.sink + lane;
+      *dst = lch[k];
     });
   }
 
@@ -1370,19 +1374,17 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_layer_kernel(RadArgs A) {
   {
     double X[4][4], Y[4][4], U[4][4], UT[4][4];
     {
-      double LiT[4][4];
-      get_m(S0, h, c, LiT);         // L^-T (M): the A^T operand of L^-1 (.)
-      get_mt(S0, h, c, X);          // L^-1 (M)
-      mprod<false>(X, X, Y, h, c);  // W = L^-T L^-1
-      get_mt(S1, h, c, X);          // C^-1 (M)
+      // L^-T stays in S0 until V = L^-1 U is formed; W = L^-T L^-1 is formed after
+      // it from the same rows (no M-layout copy of L^-T or W held across the products)
+      get_mt(S1, h, c, X);           // C^-1 (M)
       lds_fence();
-      put_m(S0, h, c, Y);            // W, row-major
       put_rows<NN>(S1, t, i, bcol);  // rows of B^T
       lds_fence();
       get_mt(S1, h, c, Y);           // B (M)
       mprod<false>(X, Y, U, h, c);   // U = C^-T B
       mprod<false>(Y, X, UT, h, c);  // U^T = B^T C^-1
-      mprod<false>(LiT, U, X, h, c); // V = L^-1 U (M) -> the record, row-major
+      get_m(S0, h, c, Y);            // L^-T (M): the A^T operand of L^-1 (.)
+      mprod<false>(Y, U, X, h, c);   // V = L^-1 U (M) -> the record, row-major
 #pragma unroll
       for (int tt = 0; tt < 4; ++tt) {
         const bool ok = grp * 4 + tt < A.nu;
@@ -1393,6 +1395,10 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_layer_kernel(RadArgs A) {
           if (ok && r < NN && c < NN) rv[oV + r * NN + c] = X[tt][q2];
         }
       }
+      get_mt(S0, h, c, X);          // L^-1 (M)
+      mprod<false>(X, X, Y, h, c);  // W = L^-T L^-1
+      lds_fence();
+      put_m(S0, h, c, Y);           // W, row-major
     }
     lds_fence();
     put_m(S1, h, c, UT);
@@ -1594,12 +1600,14 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_sweep_kernel(RadArgs A) {
     const double* lp = A.rsw + (size_t)lc * NE1 * nu;  // element e of unit v: lp[v*NE1 + e]
     double* bp = A.bsub + (size_t)lc * NB * nu;
     // the stack above this layer: R_above (packed upper, row i from j = i) and S_down
-    if (wr) {
+    {  // branch-free: the elements a lane does not own go to the sink
+      double* urow = bp + (size_t)u * NB + NN * NN + NN + sym_index<NN>(ii, ii) - ii;
       sfor<0, NN>([&](auto J) {
         constexpr int j = HD_K(J);
-        if (j >= i) bp[(size_t)u * NB + NN * NN + NN + sym_index<NN>(i, j)] = ra[j];
+        double* dst = (wr && j >= i) ? urow + j : A.sink + lane;
+        *dst = ra[j];
       });
-      bp[(size_t)u * NB + NN * NN + NN + nsym + i] = sd;
+      if (wr) bp[(size_t)u * NB + NN * NN + NN + nsym + i] = sd;
     }
     // R~, T~ (packed upper) of the four units in M layout; this unit's rows (T layout)
     double rm[4][4], tm[4][4];
@@ -1881,10 +1889,11 @@ hipError_t launch_team_layer_mfma(int nn, const LayerArgs& la, hipStream_t strea
 // radiance at each user depth (interior: I_entry e^{-|t_in - t|/|mu|} + partial).
 // ============================================================================
 template <int NN>
-__global__ __launch_bounds__(64, 2) void hd_rad_team_user_kernel(RadArgs A) {
-  __shared__ double lds[2 * kSet + 8 * 32 + 8 * 4 + 8 * 8];
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
+void hd_rad_team_user_kernel(RadArgs A) {
+  // 11.5 KB: three waves per SIMD (L^T's M layout comes straight from the record)
+  __shared__ double lds[kSet + 8 * 32 + 8 * 4 + 8 * 8];
   double* S0 = lds;          // rows of L^-T
-  double* S1 = lds + kSet;   // rows of L
   constexpr int N = 2 * NN;
   constexpr int nsym = NN * (NN + 1) / 2;
   constexpr int NE1 = rad_layer_record_doubles(NN);
@@ -1908,7 +1917,7 @@ __global__ __launch_bounds__(64, 2) void hd_rad_team_user_kernel(RadArgs A) {
   const double* rec = A.rrd + (size_t)lc * nu * NR;  // element e of unit v: rec[v * NR + e]
   auto rv = [&](int e, int tt) { return rec[(size_t)um[tt] * NR + e]; };
 
-  for (int k = lane; k < 2 * kSet; k += 64) lds[k] = 0.0;
+  for (int k = lane; k < kSet; k += 64) lds[k] = 0.0;
   lds_fence();
 
   // ---- L's rows (T layout) and L^-T's rows by the team's forward substitution ----
@@ -1924,7 +1933,6 @@ __global__ __launch_bounds__(64, 2) void hd_rad_team_user_kernel(RadArgs A) {
     double z[NN];
     team_tri_inverse_col<NN>(lrow, rdl, z);  // row i of L^-T
     put_rows<NN>(S0, t, i, z);
-    put_rows<NN>(S1, t, i, lrow);
   }
   lds_fence();
   lds_fence();
@@ -1945,7 +1953,7 @@ __global__ __launch_bounds__(64, 2) void hd_rad_team_user_kernel(RadArgs A) {
     rft[tt] = om / (1.0 - f);
     taupt[tt] = rv(oTp, tt);
   }
-  double* red = lds + 2 * kSet;  // [angle][lay | sc | x0 | th][h, parity]
+  double* red = lds + kSet;      // [angle][lay | sc | x0 | th][h, parity]
   double* aux = red + 8 * 32;     // [angle][ab | a0 | a1t | -]
   double* red2 = aux + 8 * 4;     // [angle][h, parity]
   const int a = c & 7, fam = c >> 3;
@@ -1998,7 +2006,11 @@ __global__ __launch_bounds__(64, 2) void hd_rad_team_user_kernel(RadArgs A) {
         }
         d4 p = {0.0, 0.0, 0.0, 0.0}, gq = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) x[q] = S1[tt * kTile + c * kS + h + 4 * q];  // L^T (M)
+        for (int q = 0; q < 4; ++q) {  // L^T (M): L[c][h + 4q], packed lower in the record
+          const int r = h + 4 * q;
+          const bool in = r <= c && c < NN;
+          x[q] = in ? rl(in ? c * (c + 1) / 2 + r : 0, tt) : 0.0;
+        }
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) p = __builtin_amdgcn_mfma_f64_16x16x4f64(x[s4], vm[s4], p, 0, 0, 0);
 #pragma unroll
