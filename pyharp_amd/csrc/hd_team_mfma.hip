@@ -1060,7 +1060,8 @@ __global__ __launch_bounds__(64, 2) void hd_team_mfma_sweep_lean_kernel(SweepArg
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           const int r = h + 4 * m;
-          if (ok && r < NN && c < NN) zr[r * NN + c] = zm[tt][m];
+          // branch-free: an element the lane does not own goes to the sink
+          *((ok && r < NN && c < NN) ? zr + r * NN + c : A.sink + lane) = zm[tt][m];
         }
       }
       double pm[4][4];
@@ -1607,7 +1608,7 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_sweep_kernel(RadArgs A) {
         double* dst = (wr && j >= i) ? urow + j : A.sink + lane;
         *dst = ra[j];
       });
-      if (wr) bp[(size_t)u * NB + NN * NN + NN + nsym + i] = sd;
+      *(wr ? bp + (size_t)u * NB + NN * NN + NN + nsym + i : A.sink + lane) = sd;
     }
     // R~, T~ (packed upper) of the four units in M layout; this unit's rows (T layout)
     double rm[4][4], tm[4][4];
@@ -1676,7 +1677,7 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_sweep_kernel(RadArgs A) {
     // u = A t1 + Sd
     double uv = sd;
     sfor<0, NN>([&](auto K) { uv = fma(ra[HD_K(K)], bc<HD_K(K)>(t1), uv); });
-    if (wr) bp[(size_t)u * NB + NN * NN + i] = t1;
+    *(wr ? bp + (size_t)u * NB + NN * NN + i : A.sink + lane) = t1;
     // ZT = W1^-1 T = U^-1 (L^-1 T): columns of the triangular inverses on the team
     // (lane i: row i of the transposed inverse), the products on the matrix core
     {
@@ -1722,7 +1723,8 @@ __global__ __launch_bounds__(64, 1) void hd_rad_team_sweep_kernel(RadArgs A) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int r = h + 4 * q;
-          if (ok && r < NN && c < NN) bp[(size_t)um[tt] * NB + r * NN + c] = zm[tt][q];
+          const bool own = ok && r < NN && c < NN;
+          *(own ? bp + (size_t)um[tt] * NB + r * NN + c : A.sink + lane) = zm[tt][q];
         }
       }
       mprod<false>(ram, zm, pm, h, c);  // A ZT

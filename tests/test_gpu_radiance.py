@@ -390,3 +390,22 @@ def test_team_user_kernel_matches_rolled(nstr, planck, usrtau, nwave, tmp_path):
     other = np.load(out)
     assert np.all(np.isfinite(here))
     assert margin(_col_err(here, other)) < 1e-10, _col_err(here, other)
+
+
+def test_many_user_angles_fallback_vs_oracle():
+    """More user angles than a layer record holds (nstr 18: 109): the one-lane
+    const and user-angle kernels run on the team kernels' unit-contiguous records"""
+    rng = np.random.default_rng(4242)
+    nstr, nwave, ncol, nlyr = 18, 1, 2, 4
+    prop, bc, kw = _random_case(rng, nwave, ncol, nlyr, nstr, False)
+    umu = list(np.concatenate([-np.linspace(1.0, 0.05, 60), np.linspace(0.05, 1.0, 60)]))
+    total = prop[..., 0].sum(axis=-1).min()
+    utau = [0.0, 0.37 * total, total]
+    d = _disort(nstr, nlyr, nwave, ncol, flags="usrtau,usrang,lamber,quiet", umu=umu,
+                phi=[0.0, 90.0], utau=utau)
+    flux = d.forward(torch.as_tensor(prop, device=DEV), _dev(bc)).cpu().numpy()
+    uu = d.get_rad().cpu().numpy()
+    fref, uref = disort_rad_forward(prop, bc, nstr=nstr, umu=umu, phi=[0.0, 90.0], utau=utau)
+    assert uu.shape == uref.shape
+    assert margin(_col_err(uu, uref)) < TOL, _col_err(uu, uref)
+    assert margin(rel_err(flux, fref).max()) < TOL
