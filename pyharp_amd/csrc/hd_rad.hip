@@ -600,7 +600,11 @@ HD_RUNROLL
 // per-unit adding sweep + back-substitution keeping I+/I- at every level
 // ============================================================================
 template <int NN>
-__global__ __launch_bounds__(64) void hd_rad_sweep_kernel(RadArgs A) {
+#ifndef HD_RAD_SWEEP_WAVES
+#define HD_RAD_SWEEP_WAVES 1
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HD_RAD_SWEEP_WAVES)))
+void hd_rad_sweep_kernel(RadArgs A) {
   const Quad<NN>& Qc = quad_r<NN>();
   const int u = blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= A.nu) return;
@@ -876,7 +880,11 @@ HD_RUNROLL
 }
 
 template <int NN>
-__global__ __launch_bounds__(256) void hd_rad_const_kernel(RadArgs A) {
+#ifndef HD_RAD_CONST_WAVES
+#define HD_RAD_CONST_WAVES 1
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HD_RAD_CONST_WAVES)))
+void hd_rad_const_kernel(RadArgs A) {
   const Quad<NN>& Qc = quad_r<NN>();
   const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (id >= (long)A.nu * A.nlyr) return;
@@ -1024,7 +1032,12 @@ HD_RUNROLL
 // per-(unit, user angle) source-function integration along the ray
 // ============================================================================
 template <int NN>
-__global__ __launch_bounds__(64) void hd_rad_user_kernel(RadArgs A) {
+// HD_RAD_USER_WAVES: waves per SIMD the one-lane user-angle kernel is compiled for
+#ifndef HD_RAD_USER_WAVES
+#define HD_RAD_USER_WAVES 1
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HD_RAD_USER_WAVES)))
+void hd_rad_user_kernel(RadArgs A) {
   constexpr int N = 2 * NN;
   constexpr int nsym = NN * (NN + 1) / 2;
   constexpr int oZp = nsym + NN * NN + NN, oZm = oZp + NN, oH = oZm + NN, oBt = oH + NN;

@@ -1,17 +1,16 @@
 #!/bin/bash
-# build_variant.sh NAME HD_DEVICE_HPP : libhdisort built with an alternative hd_device.hpp -> mb/NAME/libhdisort.so
+# Build libhdisort.so with extra compile flags into ab_libs/libhdisort_NAME.so (for
+# A/B runs on one box: HD_LIB_PATH=ab_libs/libhdisort_NAME.so python ...):
+#   bash scripts/ab/build_variant.sh NAME -DFLAG=VALUE ...
 set -e
-NAME=$1; HDR=$2
-D=/root/repo/mb/$NAME
-rm -rf $D; mkdir -p $D/x/csrc $D/include
-cp /root/repo/pyharp_amd/csrc/* $D/x/csrc/; cp /root/repo/include/*.h $D/include/
-cp $HDR $D/x/csrc/hd_device.hpp
-rm -f $D/x/csrc/*.o
-objs=""
-for s in hd_kernels.hip hd_team.hip hd_rad.hip hd_harp.hip hd_api.cpp; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -x hip -c $D/x/csrc/$s -o $D/$s.o &
-  objs="$objs $D/$s.o"
+NAME=$1; shift
+OUT=ab_libs/obj_$NAME; mkdir -p $OUT
+C=pyharp_amd/csrc
+for src in hd_kernels.hip hd_team.hip hd_team_mfma.hip hd_rad.hip hd_harp.hip hd_api.cpp hd_ncread.cpp hd_rad_wide.hip; do
+  extra=""; [ $src = hd_team_mfma.hip ] && extra="-mllvm -disable-machine-licm"
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -x hip "$@" $extra -c $C/$src -o $OUT/$src.o &
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/libhdisort.so $objs
-rm -f $D/*.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ab_libs/libhdisort_$NAME.so $OUT/*.o -lz
+rm -rf $OUT
+echo ab_libs/libhdisort_$NAME.so
