@@ -887,20 +887,35 @@ __global__ __launch_bounds__(64) void hd_sweep_quad_kernel(SweepArgs A) {
   double sd = g_i * top;
   double tauc = 0.0;
 
-  for (int lc = 0; lc < L; ++lc) {
+  // layer records one layer ahead: a wave walks its layers one after another, and
+  // at 16 or 20 000 solves nothing else hides a record load's latency (C1 is one wave)
+  double rn[NN], tn[NN], spn, smn, tpn;
+  auto fetch = [&](int lc) {
     const double* lb = A.scr + (size_t)lc * RL::pairs * nsc * 2;
+#pragma unroll
+    for (int j = 0; j < NN; ++j) {
+      rn[j] = lb[eoff(RL::R + sym_index<NN>(i, j))];
+      tn[j] = lb[eoff(RL::T + sym_index<NN>(i, j))];
+    }
+    spn = lb[eoff(RL::Sp + i)];
+    smn = lb[eoff(RL::Sm + i)];
+    tpn = lb[eoff(RL::Tau)];
+  };
+  fetch(0);
+  for (int lc = 0; lc < L; ++lc) {
     double* bb = A.bsub + (size_t)lc * RB::pairs * nsc * 2;
     double r[NN], tr[NN];
 #pragma unroll
     for (int j = 0; j < NN; ++j) {
-      r[j] = lb[eoff(RL::R + sym_index<NN>(i, j))];
-      tr[j] = lb[eoff(RL::T + sym_index<NN>(i, j))];
+      r[j] = rn[j];
+      tr[j] = tn[j];
     }
     const double eb = exp(-tauc * rmu0);
     const double sscale = A.beam_scale ? eb : 1.0;
-    const double spl = lb[eoff(RL::Sp + i)] * sscale;
-    const double sml = lb[eoff(RL::Sm + i)] * sscale;
-    const double taup = lb[eoff(RL::Tau)];
+    const double spl = spn * sscale;
+    const double sml = smn * sscale;
+    const double taup = tpn;
+    fetch(lc + 1 < L ? lc + 1 : lc);
 
     // level lc (top of layer lc): F_dn = rc . I+ + cs  (A symmetric: column i = row i)
     {
