@@ -268,8 +268,9 @@ HD_RUNROLL
     const double* lam = &tab_r<NN>().lam[m][0][0];
     const double seed = ylm_seed(m, mub);
     double y1 = 0.0, y2 = 0.0;  // Y_{l-1}^m(mu0), Y_{l-2}^m(mu0)
+    // Y_l^m = 0 for l < m (tables and recurrence): the pairs below m/2 add exact zeros
 #pragma nounroll
-    for (int l2 = 0; l2 < NN; ++l2) {
+    for (int l2 = m >> 1; l2 < NN; ++l2) {
       const int la = 2 * l2, lb = la + 1;
       const double ya =
           la < m ? 0.0 : (la == m ? seed : fma(c_rad.ra[m][la] * mub, y1, -c_rad.rb[m][la] * y2));
