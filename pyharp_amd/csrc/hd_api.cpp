@@ -397,7 +397,17 @@ int hd_context_create(hd_context** out, int device) {
     HD_HIP(ctx, hipSetDevice(ctx->device));
     HD_HIP(ctx, hipMalloc(&ctx->anyerr, sizeof(int)));
     HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
-    HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->lay, hipStreamNonBlocking));
+    // HD_LAY_PRIORITY=high|low (A/B): the layer-kernel stream's dispatch priority
+    // against the caller's stream, where the sweeps run
+    const char* lp = std::getenv("HD_LAY_PRIORITY");
+    if (lp && (std::strcmp(lp, "high") == 0 || std::strcmp(lp, "low") == 0)) {
+      int least = 0, greatest = 0;
+      HD_HIP(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
+      HD_HIP(ctx, hipStreamCreateWithPriority(&ctx->lay, hipStreamNonBlocking,
+                                              std::strcmp(lp, "high") == 0 ? greatest : least));
+    } else {
+      HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->lay, hipStreamNonBlocking));
+    }
     HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
     HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming));
     HD_HIP(ctx, hipMalloc(&ctx->sink, 4096 * sizeof(double)));
