@@ -389,24 +389,45 @@ def spawn_ranks(n: int, argv, env=None, program=None) -> int:
     cmd = program if program is not None else [sys.executable, os.path.abspath(__file__)] + \
         list(argv)
     procs = []
-    for r in range(n):
-        e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
-        procs.append(subprocess.Popen(cmd, env=e))
+    pending = []
+
+    def _on_term(signum, frame):  # a SIGTERM to this parent unwinds through finally
+        raise SystemExit(128 + signum)
+
+    old_term = signal.signal(signal.SIGTERM, _on_term)
     rc = 0
-    pending = list(procs)
-    while pending:
-        for p in list(pending):
-            code = p.poll()
-            if code is None:
-                continue
-            pending.remove(p)
-            code = 128 - code if code < 0 else code
-            if code and not rc:
-                rc = code
-                for q in pending:  # a failed rank would leave the others in a collective
-                    q.send_signal(signal.SIGTERM)
-        if pending:
-            time.sleep(0.05)
+    try:
+        for r in range(n):
+            e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+            procs.append(subprocess.Popen(cmd, env=e))
+            pending.append(procs[-1])
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                code = 128 - code if code < 0 else code
+                if code and not rc:
+                    rc = code
+                    for q in pending:  # a failed rank would leave the others in a collective
+                        q.send_signal(signal.SIGTERM)
+            if pending:
+                time.sleep(0.05)
+    finally:
+        # interrupted or terminated: no rank outlives this parent (they hold GPUs and
+        # would block the next run in a collective) -- SIGTERM, then SIGKILL after 10 s
+        for q in pending:
+            if q.poll() is None:
+                q.send_signal(signal.SIGTERM)
+        deadline = time.time() + 10.0
+        for q in pending:
+            try:
+                q.wait(timeout=max(0.0, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                q.kill()
+                q.wait()
+        signal.signal(signal.SIGTERM, old_term)
     return rc
 
 
@@ -583,7 +604,7 @@ def main():
                 f"nlyr={nlyr}, " + ("thermal (planck), omega=0" if lw else
                                     f"beam{' + planck' if args.planck else ''}"))
 
-    team_valu = os.environ.get("HD_TEAM_LAYER") == "valu"  # A/B switch of the team path
+    team_valu = os.environ.get("HD_AB") == "1" and os.environ.get("HD_TEAM_LAYER") == "valu"  # A/B switch of the team path
     layer_kernel = ("hd_layer_kernel" if nstr <= 16 else
                     "hd_team_layer_kernel" if team_valu else "hd_team_mfma_layer_kernel")
     mfma = nstr > 16 and not team_valu

@@ -27,7 +27,7 @@ EXPORTED = ("hd_version", "hd_last_error", "hd_context_create", "hd_context_dest
             "hd_context_set_chunk", "hd_context_set_timing", "hd_context_set_max_sweeps",
             "hd_context_get_timing",
             "hd_context_reserve", "hd_solve", "hd_solve_band", "hd_solve_host",
-            "hd_solve_band_host", "hd_solve_radiance", "hd_quadrature")
+            "hd_solve_band_host", "hd_solve_radiance", "hd_quadrature", "hd_chunk_solves")
 
 # every symbol include/hdharp.h declares (harp-side steps around the solve)
 HARP_EXPORTED = ("hd_attenuate", "hd_band_optics", "hd_band_loop_optics", "hd_rfm_attenuate",
@@ -109,6 +109,8 @@ def load(path: str = LIB_PATH):
     lib.hd_context_set_max_sweeps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.hd_context_get_timing.argtypes = [ctypes.c_void_p, ctypes.POINTER(HdTiming)]
     lib.hd_context_reserve.argtypes = [ctypes.c_void_p, ctypes.POINTER(HdConfig), ctypes.c_long]
+    lib.hd_chunk_solves.restype = ctypes.c_long
+    lib.hd_chunk_solves.argtypes = [ctypes.POINTER(HdConfig), ctypes.c_long]
     lib.hd_solve.argtypes = [ctypes.c_void_p, ctypes.POINTER(HdConfig), ctypes.POINTER(HdInputs),
                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.hd_solve_band.argtypes = [ctypes.c_void_p, ctypes.POINTER(HdConfig),
@@ -245,3 +247,13 @@ def quadrature(nstr: int):
     w = (ctypes.c_double * nn)()
     check(load().hd_quadrature(int(nstr), mu, w))
     return list(mu), list(w)
+
+
+def chunk_solves(nstr: int, nlyr: int, nsolve: int, planck: bool = False) -> int:
+    """hd_chunk_solves: solves per internal chunk under the automatic chunking."""
+    cfg = HdConfig(nstr=int(nstr), nmom=int(nstr), nlyr=int(nlyr), nprop=2 + int(nstr),
+                   flags=HD_FLAG_LAMBER | HD_FLAG_ONLYFL | (HD_FLAG_PLANCK if planck else 0))
+    n = load().hd_chunk_solves(ctypes.byref(cfg), int(nsolve))
+    if n < 0:
+        raise RuntimeError(f"hd_chunk_solves: bad args (nstr={nstr}, nlyr={nlyr}, nsolve={nsolve})")
+    return n

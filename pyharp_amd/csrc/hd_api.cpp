@@ -48,6 +48,11 @@ struct hd_context {
   // nstr 4 / 8: the sweep in NN-lane teams (hd_sweep_quad_kernel) for chunks of at
   // most kQuadMaxSolves solves (-1, the default), always (1) or never (0): HD_SWEEP_QUAD
   int quad = -1;
+  // nstr 16: the adding sweep with the stack state in LDS (hd_sweep_lean_kernel,
+  // two waves per SIMD) -- off by default: 1 024 waves per chunk spread one per SIMD
+  // and each runs 1.85 ms against hd_sweep_kernel's 1.4 (C4 12.38 vs 12.77 M,
+  // profiles/r05/lean8_ab.txt); HD_AB=1 HD_SWEEP_LEAN8=1 picks it
+  int lean8 = 0;
   // true while a solve enqueues into a capturing stream: scratch may not grow then
   bool capturing = false;
   std::string err;
@@ -208,6 +213,10 @@ int ensure_rad_tables(hd_context* ctx) {
   return HD_OK;
 }
 
+// team path: below this many solves per chunk a chunk's sweep (16 lanes per solve)
+// no longer fills the SIMDs it could share with the next chunk's layer kernel
+constexpr long kTeamMinChunk = 2048;
+
 long auto_chunk(long nsolve, int nn, int nlyr, bool planck) {
   // NN <= 8: the sweep runs one lane per solve at one wave per SIMD (its
   // register file is full), so a chunk of 65 536 solves is one wave on each of
@@ -223,7 +232,13 @@ long auto_chunk(long nsolve, int nn, int nlyr, bool planck) {
     const double per = 8.0 * (double)hd::scratch_doubles_per_solve(nn, nlyr, planck);
     target = std::min<long>(262144, std::max<long>(16384, (long)(budget / per)));
   }
-  if (nsolve <= target) return nsolve;
+  if (nsolve <= target) {
+    // team path: a call that fits one chunk still takes two, so the second chunk's
+    // layer kernel runs beside the first one's sweep (the 8-GPU C5 rank shape is
+    // 8 000 solves: one chunk left the sweep wholly exposed)
+    if (nn > hd::kMaxRegNN && nsolve >= 2 * kTeamMinChunk) return (nsolve + 1) / 2;
+    return nsolve;
+  }
   const long n = (nsolve + target - 1) / target;
   return (nsolve + n - 1) / n;
 }
@@ -389,25 +404,16 @@ int hd_context_create(hd_context** out, int device) {
     return fail(nullptr, HD_EINVAL, "hd_context_create: device %d out of range (%d)", device,
                 ndev);
   hd_context* ctx = new hd_context();
-  if (const char* e = std::getenv("HD_JACOBI_WARM")) ctx->warm = std::atoi(e) != 0;
-  if (const char* e = std::getenv("HD_TEAM_SWEEP_LEAN")) ctx->lean = std::atoi(e) != 0;
-  if (const char* e = std::getenv("HD_SWEEP_QUAD")) ctx->quad = std::atoi(e) < 0 ? -1 : std::atoi(e) != 0;
+  if (const char* e = hd::ab_env("HD_JACOBI_WARM")) ctx->warm = std::atoi(e) != 0;
+  if (const char* e = hd::ab_env("HD_TEAM_SWEEP_LEAN")) ctx->lean = std::atoi(e) != 0;
+  if (const char* e = hd::ab_env("HD_SWEEP_QUAD")) ctx->quad = std::atoi(e) < 0 ? -1 : std::atoi(e) != 0;
+  if (const char* e = hd::ab_env("HD_SWEEP_LEAN8")) ctx->lean8 = std::atoi(e) != 0;
   ctx->device = device;
   auto init = [ctx]() -> int {
     HD_HIP(ctx, hipSetDevice(ctx->device));
     HD_HIP(ctx, hipMalloc(&ctx->anyerr, sizeof(int)));
     HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
-    // HD_LAY_PRIORITY=high|low (A/B): the layer-kernel stream's dispatch priority
-    // against the caller's stream, where the sweeps run
-    const char* lp = std::getenv("HD_LAY_PRIORITY");
-    if (lp && (std::strcmp(lp, "high") == 0 || std::strcmp(lp, "low") == 0)) {
-      int least = 0, greatest = 0;
-      HD_HIP(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
-      HD_HIP(ctx, hipStreamCreateWithPriority(&ctx->lay, hipStreamNonBlocking,
-                                              std::strcmp(lp, "high") == 0 ? greatest : least));
-    } else {
-      HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->lay, hipStreamNonBlocking));
-    }
+    HD_HIP(ctx, hipStreamCreateWithFlags(&ctx->lay, hipStreamNonBlocking));
     HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
     HD_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming));
     HD_HIP(ctx, hipMalloc(&ctx->sink, 4096 * sizeof(double)));
@@ -519,12 +525,19 @@ int hd_context_reserve(hd_context* ctx, const hd_config* cfg, long nsolve) {
   const int nslot_max = hd::band_slots(1);
   const size_t band_extra = std::max(4 * (size_t)c1 + (size_t)((c1 + 63) / 64) * nslot_max *
                                                           2 * (size_t)(cfg->nlyr + 1),
-                                     (size_t)c1 * 2 * (size_t)(cfg->nlyr + 1));
+                                     2 * (size_t)c1 * 2 * (size_t)(cfg->nlyr + 1));
   int rc = ensure_scratch(ctx, per * c1 + band_extra);
   if (rc) return rc;
   rc = ensure_tables(ctx);
   if (rc) return rc;
   return ensure_status(ctx, (size_t)nsolve);
+}
+
+long hd_chunk_solves(const hd_config* cfg, long nsolve) {
+  if (!cfg || nsolve < 0 || cfg->nstr < 2 || cfg->nstr % 2 || cfg->nstr / 2 > hd::kMaxNN ||
+      cfg->nlyr < 1)
+    return -1;
+  return auto_chunk(nsolve, cfg->nstr / 2, cfg->nlyr, (cfg->flags & HD_FLAG_PLANCK) != 0);
 }
 
 int hd_quadrature(int nstr, double* mu, double* w) {
@@ -562,7 +575,9 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
   const int nslot = band ? hd::band_slots(in->nwave) : 0;
   size_t band_extra = 0;
   if (band && reg) band_extra = 4 * (size_t)chunk + (size_t)((chunk + 63) / 64) * nslot * nlev2;
-  if (band && !reg && !flux) band_extra = (size_t)chunk * nlev2;
+  // team path without caller fluxes: two chunk flux buffers (the band reduce of chunk
+  // k runs on the side stream beside sweep k+1)
+  if (band && !reg && !flux) band_extra = 2 * (size_t)chunk * nlev2;
   rc = ensure_scratch(ctx, per * chunk + band_extra);
   if (rc) return rc;
   rc = ensure_tables(ctx);
@@ -625,18 +640,19 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
   }
   double* fsurf_b[2] = {nullptr, nullptr};
   double* part = nullptr;
-  double* fchunk = nullptr;
+  double* fchunk_b[2] = {nullptr, nullptr};
   if (band && reg) {
     fsurf_b[0] = band_q;
     fsurf_b[1] = band_q + 2 * (size_t)chunk;
     part = band_q + 4 * (size_t)chunk;
-  } else if (band) {
-    fchunk = flux ? nullptr : band_q;
+  } else if (band && !flux) {
+    fchunk_b[0] = band_q;
+    fchunk_b[1] = band_q + (size_t)chunk * nlev2;
   }
-  auto band_args = [&](long s0, int nsc) {
+  auto band_args = [&](long s0, int nsc, int b) {
     hd::BandArgs ba{};
     ba.part = part;
-    ba.fchunk = part ? nullptr : (flux ? flux + (size_t)s0 * nlev2 : fchunk);
+    ba.fchunk = part ? nullptr : (flux ? flux + (size_t)s0 * nlev2 : fchunk_b[b]);
     ba.wts = band->weight;
     ba.bflux = band->bflux;
     ba.s0 = s0;
@@ -744,6 +760,7 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
     sa.beam_scale = beam_in_sweep ? 1 : 0;
     sa.lean = ctx->lean;
     sa.quad = ctx->quad;
+    sa.lean8 = ctx->lean8;
     if (band && reg) {
       sa.wts = band->weight;
       sa.part = part;
@@ -751,7 +768,7 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
       sa.nslot = nslot;
       sa.rsteps = hd::band_steps(in->nwave);
     } else if (band && !flux) {
-      sa.flux = fchunk;
+      sa.flux = fchunk_b[buf];
       sa.flux_local = 1;
     }
     hipEvent_t* ev = nullptr;
@@ -777,7 +794,7 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
       if (e == hipSuccess) e = hd::launch_sweep_nn(nn, sa, stream);
       if (ev) HD_HIP(ctx, hipEventRecord(ev[3], stream));
       if (e == hipSuccess) e = hd::launch_backsub_nn(nn, sa, stream, true);
-      if (e == hipSuccess && band) e = hd::launch_band_reduce(band_args(s0, nsc), stream);
+      if (e == hipSuccess && band) e = hd::launch_band_reduce(band_args(s0, nsc, buf), stream);
     } else if (reg) {
       // layer kernel k on `lay`: its inputs (prologue k) are in, and sweep k-2,
       // the last reader of layer records[buf], is done
@@ -803,15 +820,25 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
       HD_HIP(ctx, hipEventRecord(ctx->ev_layer[buf], ctx->lay));
       if (e == hipSuccess) {
         HD_HIP(ctx, hipStreamWaitEvent(stream, ctx->ev_layer[buf], 0));
+        // the chunk flux buffer[buf] is free once band reduce k-2 (its reader) is done
+        if (band && k >= 2) HD_HIP(ctx, hipStreamWaitEvent(stream, ctx->ev_back[buf], 0));
         if (ev) HD_HIP(ctx, hipEventRecord(ev[2], stream));
         e = hd::launch_team_sweep_nn(nn, sa, stream);
         if (ev) HD_HIP(ctx, hipEventRecord(ev[3], stream));
       }
-      if (e == hipSuccess && band) e = hd::launch_band_reduce(band_args(s0, nsc), stream);
       HD_HIP(ctx, hipEventRecord(ctx->ev_sweep[buf], stream));
+      // the band reduce of chunk k on the side stream: on the caller's stream it sat
+      // between sweep k and sweep k+1 waiting for SIMDs the co-running layer kernel
+      // held (6.4 ms average per 11 us launch, profiles/r04/c5_kernel_stats_final.csv);
+      // the reduces stay in chunk order (bflux accumulates chunk by chunk)
+      if (e == hipSuccess && band) {
+        HD_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_sweep[buf], 0));
+        e = hd::launch_band_reduce(band_args(s0, nsc, buf), ctx->side);
+        HD_HIP(ctx, hipEventRecord(ctx->ev_back[buf], ctx->side));
+      }
     } else {
       e = hd::launch_solve_chunk_team(nn, nullptr, nullptr, la, sa, stream, ev);
-      if (e == hipSuccess && band) e = hd::launch_band_reduce(band_args(s0, nsc), stream);
+      if (e == hipSuccess && band) e = hd::launch_band_reduce(band_args(s0, nsc, buf), stream);
     }
     if (e != hipSuccess) return fail(ctx, HD_EHIP, "hd_solve: launch failed: %s", hipGetErrorString(e));
     if (reg && !single) {
@@ -836,14 +863,14 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
       // hidden under the next layer kernel stays ahead (profiles/r02_tail_ab/)
       const bool tail = s1 >= nsolve || (nsolve + chunk - 1) / chunk <= 3;
       e = hd::launch_backsub_nn(nn, sa, ctx->side, tail);
-      if (e == hipSuccess && band) e = hd::launch_band_reduce(band_args(s0, nsc), ctx->side);
+      if (e == hipSuccess && band) e = hd::launch_band_reduce(band_args(s0, nsc, buf), ctx->side);
       if (e != hipSuccess)
         return fail(ctx, HD_EHIP, "hd_solve: back-substitution launch failed: %s",
                     hipGetErrorString(e));
       HD_HIP(ctx, hipEventRecord(ctx->ev_back[buf], ctx->side));
     }
   }
-  if (reg && !single) {  // the caller's stream sees every chunk's fluxes complete
+  if ((reg && !single) || (team_pipe && band)) {  // every chunk's fluxes complete
     for (long b = 0; b < std::min<long>(k, 2); ++b)
       HD_HIP(ctx, hipStreamWaitEvent(stream, ctx->ev_back[b], 0));
   }

@@ -530,7 +530,10 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
   for (int i = 0; i < NN; ++i) out.put(RL::Sm + i, smv[i]);
   out.close(RL::Sm + NN - 1);
   out.put(RL::Tau, taup);
-  out.close(RL::Tau);
+  // the pad after tau': the layer's direct-beam transmission e^(-tau'/mu0) (1
+  // without a beam), from which hd_sweep_lean_kernel carries the beam down as a
+  // running product instead of an exp of the running depth
+  out.put(RL::Tau + 1, beam ? e0 : 1.0);
   if (!isfinite(chk + taup)) st |= kStNonFinite;
   if (st) {
     atomicOr(&A.status[s], st);
@@ -791,6 +794,355 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
       fo[1] = f1;
     }
     if (A.fsurf) {  // band epilogue: the back-substitution sums the surface level too
+      A.fsurf[sl] = f0;
+      A.fsurf[nsc + sl] = f1;
+    }
+    chk += f0 + f1;
+  }
+  A.xsurf[sl] = x;
+  if (!isfinite(chk)) st |= kStNonFinite;
+  if (st) {
+    atomicOr(&A.status[s], st);
+    if (st & 0x0F) atomicOr(A.anyerr, 1);
+  }
+}
+
+// ============================================================================
+// K2 for nstr 16 (NN = 8) at two waves per SIMD: the adding sweep of
+// hd_sweep_kernel with the stack state (Ra packed upper, Sd) parked in LDS
+// between its uses instead of in registers, and the layer's R~ / T~ read from
+// the record where they are used.  hd_sweep_kernel holds Ra, R~, T~, W1 and
+// M1/P together (492 VGPRs: one wave per SIMD, VALU busy half the time on its
+// dependency chains); here at most W1 and one symmetric 8 x 8 matrix are live
+// (<= 256 VGPRs), so two sweep waves share a SIMD and fill each other's stalls.
+//   W1 = I - R~ Ra          Ra streamed from LDS, packed pair by pair
+//   t1 = W1^-1 (R~ Sd + S+) pivot-free LU (hd_sweep_kernel's)
+//   u  = Ra t1 + Sd         -> LDS (over Sd)
+//   ZT = W1^-1 T~           column by column, stored
+//   M1 = Ra W1^-1           row by row, upper triangle kept (M1 is symmetric)
+//   Ra <- R~ + T~ (M1 T~)   column by column -> LDS; Sd <- T~ u + S-
+// The level fluxes' row vector rc = 2 pi Ra g of the next level is formed while
+// Ra is written and stored into that level's record.  Records as hd_sweep_kernel
+// (RecL in, RecB out): the back-substitution kernels are shared.
+// ============================================================================
+template <int NN>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+void hd_sweep_lean_kernel(SweepArgs A) {
+  static_assert(NN % 2 == 0, "even NN: Sd fills whole pairs");
+  constexpr int nsym = NN * (NN + 1) / 2;
+  constexpr int kRaP = (nsym + 1) / 2;  // LDS pairs of packed Ra
+  constexpr int kSdP = NN / 2;          // then Sd (or u)
+  __shared__ double2 stk[kRaP + kSdP][64];
+  const Quad<NN>& Qc = quad<NN>();
+  const int lt = (int)threadIdx.x;
+  const long sl = (long)blockIdx.x * blockDim.x + lt;
+  if (sl >= A.nsc) return;  // one wave per block: no barrier below
+  const long s = solve_of(A.s0 + sl, A.cmaj, A.nwave, A.ncol);
+  const int L = A.nlyr;
+  const size_t nsc = A.nsc;
+  using RL = RecL<NN>;
+  using RB = RecB<NN>;
+  int st = 0;
+
+  const double twopi = 2.0 * kPi;
+  double f0mu0;
+  {
+    const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
+    const double fb = A.fbeam ? A.fbeam[s] : 0.0;
+    f0mu0 = fb > 0.0 && mu0 > 0.0 ? fb * mu0 : 0.0;
+  }
+
+  // packed element e of Ra / element i of Sd in this lane's LDS slots
+  auto ra_at = [&](int e) {
+    const double2 q = stk[e >> 1][lt];
+    return (e & 1) ? q.y : q.x;
+  };
+  auto sd_load = [&](double (&v)[NN]) {
+#pragma unroll
+    for (int p = 0; p < kSdP; ++p) {
+      const double2 q = stk[kRaP + p][lt];
+      v[2 * p] = q.x;
+      v[2 * p + 1] = q.y;
+    }
+  };
+  auto sd_store = [&](const double (&v)[NN]) {
+#pragma unroll
+    for (int p = 0; p < kSdP; ++p) stk[kRaP + p][lt] = make_double2(v[2 * p], v[2 * p + 1]);
+  };
+  {
+    double top = A.fisot ? A.fisot[s] : 0.0;
+    if (A.planck) top += A.planckv[(size_t)(L + 2) * nsc + sl];
+    double sd0[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) sd0[i] = Qc.g[i] * top;
+#pragma unroll
+    for (int p = 0; p < kRaP; ++p) stk[p][lt] = make_double2(0.0, 0.0);
+    sd_store(sd0);
+    // level 0 (top): Ra = 0, so rc = 0 and cs = g . Sd
+    PairOut bp{reinterpret_cast<double2*>(A.bsub) + sl, nsc, 0.0};
+    double cs = 0.0;
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      bp.put(RB::Rc + i, 0.0);
+      cs = fma(Qc.g[i], sd0[i], cs);
+    }
+    bp.close(RB::Rc + NN - 1);
+    bp.put(RB::Cs, fma(twopi, cs, f0mu0));
+    bp.close(RB::Cs);
+  }
+  double eb = 1.0;  // direct beam at the layer top: running product of transmissions
+
+  for (int lc = 0; lc < L; ++lc) {
+    const double2* lp = reinterpret_cast<const double2*>(A.scr) + (size_t)lc * RL::pairs * nsc + sl;
+    auto rec = [&](int e) { return pair_get(lp, nsc, e); };
+    PairOut bp{reinterpret_cast<double2*>(A.bsub) + (size_t)lc * RB::pairs * nsc + sl, nsc, 0.0};
+    const double sscale = A.beam_scale ? eb : 1.0;
+
+    // ---- W1 = I - R Ra ; v1 = R Sd + S+  (each packed element of Ra once, in
+    //      increasing k for every W1[i][j]: hd_sweep_kernel's fma order) ----
+    double w1[NN][NN], t1[NN];
+    {
+      double rl[NN][NN];  // R~ upper
+      {
+        int e = 0;
+#pragma unroll
+        for (int i = 0; i < NN; ++i)
+#pragma unroll
+          for (int j = i; j < NN; ++j) rl[i][j] = rec(RL::R + (e++));
+      }
+#pragma unroll
+      for (int i = 0; i < NN; ++i)
+#pragma unroll
+        for (int j = 0; j < NN; ++j) w1[i][j] = (i == j) ? 1.0 : 0.0;
+      int e = 0;
+#pragma unroll
+      for (int a = 0; a < NN; ++a)
+#pragma unroll
+        for (int b = a; b < NN; ++b, ++e) {
+          const double x = ra_at(e);  // Ra[a][b] = Ra[b][a]
+#pragma unroll
+          for (int i = 0; i < NN; ++i) {
+            w1[i][b] = fma(-HD_SYM(rl, i, a), x, w1[i][b]);
+            if (a != b) w1[i][a] = fma(-HD_SYM(rl, i, b), x, w1[i][a]);
+          }
+        }
+      double sd[NN];
+      sd_load(sd);
+#pragma unroll
+      for (int i = 0; i < NN; ++i) {
+        double t = rec(RL::Sp + i) * sscale;
+#pragma unroll
+        for (int k = 0; k < NN; ++k) t = fma(HD_SYM(rl, i, k), sd[k], t);
+        t1[i] = t;
+      }
+    }
+    HD_PHASE();
+    // LU without pivoting, reciprocal pivots on the diagonal (hd_sweep_kernel's)
+#pragma unroll
+    for (int k = 0; k < NN; ++k) {
+      const double piv = w1[k][k];
+      if (!(fabs(piv) > 1.0e-12)) st |= kStPivot;
+      const double rp = rcp_nr(piv);
+      w1[k][k] = rp;
+#pragma unroll
+      for (int i = k + 1; i < NN; ++i) {
+        const double l = w1[i][k] * rp;
+        w1[i][k] = l;
+#pragma unroll
+        for (int j = k + 1; j < NN; ++j) w1[i][j] = fma(-l, w1[k][j], w1[i][j]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int k = 0; k < i; ++k) t1[i] = fma(-w1[i][k], t1[k], t1[i]);
+#pragma unroll
+    for (int i = NN - 1; i >= 0; --i) {
+#pragma unroll
+      for (int k = i + 1; k < NN; ++k) t1[i] = fma(-w1[i][k], t1[k], t1[i]);
+      t1[i] *= w1[i][i];
+    }
+#pragma unroll
+    for (int i = 0; i < NN; ++i) bp.put(RB::Tv + i, t1[i]);
+    bp.close(RB::Tv + NN - 1);
+    // u = Ra t1 + Sd -> LDS (Sd is not needed again)
+    {
+      double u[NN];
+      sd_load(u);
+      int e = 0;
+#pragma unroll
+      for (int a = 0; a < NN; ++a)
+#pragma unroll
+        for (int b = a; b < NN; ++b, ++e) {
+          const double x = ra_at(e);
+          u[a] = fma(x, t1[b], u[a]);
+          if (a != b) u[b] = fma(x, t1[a], u[b]);
+        }
+      sd_store(u);
+    }
+    HD_PHASE();
+    // ---- ZT = W1^-1 T~ column by column (stored) ----
+    {
+      double tl[NN][NN];
+      {
+        int e = 0;
+#pragma unroll
+        for (int i = 0; i < NN; ++i)
+#pragma unroll
+          for (int j = i; j < NN; ++j) tl[i][j] = rec(RL::T + (e++));
+      }
+#pragma unroll
+      for (int j = 0; j < NN; ++j) {
+        double x[NN];
+#pragma unroll
+        for (int i = 0; i < NN; ++i) x[i] = HD_SYM(tl, i, j);
+#pragma unroll
+        for (int i = 0; i < NN; ++i)
+#pragma unroll
+          for (int k = 0; k < i; ++k) x[i] = fma(-w1[i][k], x[k], x[i]);
+#pragma unroll
+        for (int i = NN - 1; i >= 0; --i) {
+#pragma unroll
+          for (int k = i + 1; k < NN; ++k) x[i] = fma(-w1[i][k], x[k], x[i]);
+          x[i] *= w1[i][i];
+        }
+#pragma unroll
+        for (int i = 0; i < NN; ++i) bp.put(RB::Z + j * NN + i, x[i]);
+      }
+      bp.close(RB::Z + NN * NN - 1);
+    }
+    HD_PHASE();
+    // ---- M1 = Ra W1^-1 (upper): row r solves x W1 = Ra[r,:] -> (x L) U = a ----
+    double m1[NN][NN];
+    {
+#pragma unroll
+      for (int r = 0; r < NN; ++r) {
+        double x[NN];
+#pragma unroll
+        for (int j = 0; j < NN; ++j) {  // z U = a (forward over columns)
+          double t = ra_at(sym_index<NN>(r, j));
+#pragma unroll
+          for (int k = 0; k < j; ++k) t = fma(-x[k], w1[k][j], t);
+          x[j] = t * w1[j][j];
+        }
+#pragma unroll
+        for (int j = NN - 1; j >= r; --j) {  // x L = z (backward, unit L): j >= r only
+          double t = x[j];
+#pragma unroll
+          for (int k = j + 1; k < NN; ++k) t = fma(-x[k], w1[k][j], t);
+          x[j] = t;
+        }
+#pragma unroll
+        for (int j = r; j < NN; ++j) m1[r][j] = x[j];
+      }
+    }
+    HD_PHASE();
+    // ---- Ra <- R~ + T~ P, P = M1 T~ (column by column) ; Sd <- T~ u + S- ----
+    {
+      double tl[NN][NN];
+      {
+        int e = 0;
+#pragma unroll
+        for (int i = 0; i < NN; ++i)
+#pragma unroll
+          for (int j = i; j < NN; ++j) tl[i][j] = rec(RL::T + (e++));
+      }
+      double rcn[NN];
+#pragma unroll
+      for (int i = 0; i < NN; ++i) rcn[i] = 0.0;
+      double* ldsd = reinterpret_cast<double*>(&stk[0][0]);
+#pragma unroll
+      for (int j = 0; j < NN; ++j) {
+        double pc[NN];
+#pragma unroll
+        for (int k = 0; k < NN; ++k) {
+          double t = 0.0;
+#pragma unroll
+          for (int m = 0; m < NN; ++m) t = fma(HD_SYM(m1, k, m), HD_SYM(tl, m, j), t);
+          pc[k] = t;
+        }
+#pragma unroll
+        for (int i = 0; i <= j; ++i) {
+          const int e = sym_index<NN>(i, j);
+          double t = rec(RL::R + e);
+#pragma unroll
+          for (int k = 0; k < NN; ++k) t = fma(HD_SYM(tl, i, k), pc[k], t);
+          ldsd[((e >> 1) * 64 + lt) * 2 + (e & 1)] = t;
+          rcn[i] = fma(t, Qc.g[j], rcn[i]);
+          if (i != j) rcn[j] = fma(t, Qc.g[i], rcn[j]);
+        }
+      }
+      double u[NN], sdn[NN];
+      sd_load(u);
+      double cs = 0.0;
+#pragma unroll
+      for (int i = 0; i < NN; ++i) {
+        double t = rec(RL::Sm + i) * sscale;
+#pragma unroll
+        for (int k = 0; k < NN; ++k) t = fma(HD_SYM(tl, i, k), u[k], t);
+        sdn[i] = t;
+        cs = fma(Qc.g[i], t, cs);
+      }
+      sd_store(sdn);
+      eb *= rec(RL::Tau + 1);
+      if (lc + 1 < L) {  // level lc+1 (top of layer lc+1): F_dn = rc . I+ + cs
+        PairOut bn{reinterpret_cast<double2*>(A.bsub) + (size_t)(lc + 1) * RB::pairs * nsc + sl,
+                   nsc, 0.0};
+#pragma unroll
+        for (int i = 0; i < NN; ++i) bn.put(RB::Rc + i, twopi * rcn[i]);
+        bn.close(RB::Rc + NN - 1);
+        bn.put(RB::Cs, fma(twopi, cs, f0mu0 * eb));
+        bn.close(RB::Cs);
+      }
+    }
+    HD_PHASE();
+  }
+
+  // ---- Lambertian surface: I+ = g x (hd_sweep_kernel's arithmetic) ----
+  double ra[NN][NN], sd[NN];
+  {
+    int e = 0;
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int j = i; j < NN; ++j) ra[i][j] = ra_at(e++);
+    sd_load(sd);
+  }
+  // (surface inputs read here: nothing of them is live across the layer loop)
+  const double alb = A.albedo ? A.albedo[s] : 0.0;
+  if (!(alb >= 0.0) || !(alb <= 1.0)) st |= kStBadInput;
+  const double bsurf = A.planck ? A.planckv[(size_t)(L + 1) * nsc + sl] : 0.0;
+  const bool beam = f0mu0 > 0.0;
+  double gsd = 0.0, grg = 0.0;
+#pragma unroll
+  for (int i = 0; i < NN; ++i) {
+    gsd += Qc.g[i] * sd[i];
+#pragma unroll
+    for (int j = 0; j < NN; ++j) grg += Qc.g[i] * HD_SYM(ra, i, j) * Qc.g[j];
+  }
+  double esurf = (1.0 - alb) * bsurf;
+  const double dirsurf = f0mu0 * eb;
+  if (beam) esurf += alb * dirsurf / kPi;
+  const double x = (2.0 * alb * gsd + esurf) / (1.0 - 2.0 * alb * grg);
+  double chk = 0.0;
+  {
+    double up = 0.0, dn = 0.0;
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      const double ipi = Qc.g[i] * x;
+      up += Qc.g[i] * ipi;
+      double t = sd[i];
+#pragma unroll
+      for (int j = 0; j < NN; ++j) t += HD_SYM(ra, i, j) * (Qc.g[j] * x);
+      dn += Qc.g[i] * t;
+    }
+    const double f0 = twopi * up, f1 = twopi * dn + dirsurf;
+    if (A.flux) {
+      double* fo = A.flux + (size_t)s * (L + 1) * 2;
+      fo[0] = f0;
+      fo[1] = f1;
+    }
+    if (A.fsurf) {
       A.fsurf[sl] = f0;
       A.fsurf[nsc + sl] = f1;
     }
@@ -1373,6 +1725,13 @@ static void launch_sweep(const SweepArgs& sa, hipStream_t stream) {
     if (sa.quad > 0 || (sa.quad < 0 && sa.nsc <= kQuadMaxSolves)) {  // NN-lane teams
       hipLaunchKernelGGL(hd_sweep_quad_kernel<NN>, dim3((unsigned)((sa.nsc * NN + 63) / 64)),
                          dim3(64), 0, stream, sa);
+      return;
+    }
+  }
+  if constexpr (NN == 8) {
+    if (sa.lean8) {
+      hipLaunchKernelGGL(hd_sweep_lean_kernel<NN>, dim3((unsigned)((sa.nsc + 63) / 64)), dim3(64),
+                         0, stream, sa);
       return;
     }
   }

@@ -3,6 +3,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "hd_device.hpp"
 
 namespace hd {
@@ -177,6 +179,9 @@ struct SweepArgs {
   // register path, nstr 4 / 8: the sweep in NN-lane teams (hd_sweep_quad_kernel):
   // 1 on, 0 off, -1 for chunks of at most kQuadMaxSolves solves
   int quad;
+  // register path, nstr 16: the adding sweep with the stack state in LDS
+  // (hd_sweep_lean_kernel, two waves per SIMD) instead of hd_sweep_kernel
+  int lean8;
 };
 
 // chunk epilogue of the fused band sum: bflux[c] (=|+=) sum of the chunk's
@@ -248,6 +253,15 @@ inline int band_steps(int nwave) {
   int k = 0;
   while ((1 << k) < (nwave < 64 ? nwave : 64)) ++k;
   return k;
+}
+// A/B switches of the kernel variants (HD_JACOBI_WARM, HD_TEAM_SWEEP_LEAN, HD_SWEEP_QUAD,
+// HD_SWEEP_LEAN8, HD_RAD_USER, HD_TEAM_LAYER, HD_TEAM_SWEEP) are read only when the
+// single opt-in HD_AB=1 is set too: a stray variable in a user's environment never
+// changes which kernel runs (or the bits of the result).  Tests and the A/B scripts set it.
+inline const char* ab_env(const char* name) {
+  const char* on = std::getenv("HD_AB");
+  if (!on || on[0] != '1' || on[1] != '\0') return nullptr;
+  return std::getenv(name);
 }
 // record an error for hd_last_error(NULL) (entry points without a context); returns code
 int set_global_error(int code, const char* fmt, ...);

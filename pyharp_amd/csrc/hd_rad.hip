@@ -1544,7 +1544,7 @@ hipError_t upload_rad_tables(const QuadHost* per_nn) {
 // HD_RAD_USER=rolled: nstr 18..32 user angles by the one-lane-per-(unit, angle) kernel
 static bool rad_user_rolled() {
   static const bool v = [] {
-    const char* e = std::getenv("HD_RAD_USER");
+    const char* e = ab_env("HD_RAD_USER");
     return e && std::strcmp(e, "rolled") == 0;
   }();
   return v;

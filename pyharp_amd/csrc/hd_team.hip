@@ -581,7 +581,7 @@ hipError_t upload_quad_tables_team(const QuadHost* per_nn /* [kMaxNN], index nn-
 // default is the MFMA one (hd_team_mfma.hip)
 static bool team_layer_valu() {
   static const bool v = [] {
-    const char* e = std::getenv("HD_TEAM_LAYER");
+    const char* e = ab_env("HD_TEAM_LAYER");
     return e && std::strcmp(e, "valu") == 0;
   }();
   return v;
@@ -591,7 +591,7 @@ static bool team_layer_valu() {
 // the MFMA one (hd_team_mfma.hip)
 static bool team_sweep_valu() {
   static const bool v = [] {
-    const char* e = std::getenv("HD_TEAM_SWEEP");
+    const char* e = ab_env("HD_TEAM_SWEEP");
     return e && std::strcmp(e, "valu") == 0;
   }();
   return v;

@@ -82,6 +82,55 @@ _BC_KEYS = ("fbeam", "umu0", "albedo", "btemp", "ttemp", "temis", "fisot")
 _BC_IGNORED = ("phi0",)  # azimuth of the beam: used by the radiances only
 
 
+def night_side_beam(bc: Dict[str, torch.Tensor], mode: str = "dark",
+                    umu0_min: float = 1.0e-3) -> Dict[str, torch.Tensor]:
+    """Boundary conditions a GCM-style caller can pass for a whole globe.
+
+    The solver takes umu0 as given, as pydisort's forward hands it to cdisort, whose
+    input check (c_chekin) rejects a beam (fbeam > 0) with umu0 outside (0, 1]: such a
+    solve is flagged HD_STATUS_BAD_INPUT and a synchronous call fails.  A caller that
+    passes one fbeam with cos(zenith) over day and night side picks a convention here:
+
+      mode="dark"  -- fbeam = 0 where umu0 <= 0 (no direct beam on the night side;
+                      umu0 there is then not read);
+      mode="clamp" -- umu0 = max(umu0, umu0_min) where fbeam > 0 (harp's legacy driver
+                      floored umu0 at 1e-3 before calling cdisort,
+                      src/rtsolver/rt_solver_disort.cpp_:80).
+
+    Returns a new dict (the caller's tensors are not modified); umu0 > 1 stays an
+    error in both modes."""
+    if mode not in ("dark", "clamp"):
+        raise ValueError(f"night_side_beam: mode must be 'dark' or 'clamp', got {mode!r}")
+    out = dict(bc)
+    if "fbeam" not in bc or "umu0" not in bc or bc["fbeam"] is None or bc["umu0"] is None:
+        return out
+    fb = torch.as_tensor(bc["fbeam"])
+    mu = torch.as_tensor(bc["umu0"])
+    if mode == "dark":
+        fb, mu = torch.broadcast_tensors(fb, mu)
+        out["fbeam"] = torch.where(mu > 0.0, fb, torch.zeros_like(fb))
+    else:
+        fb, mu = torch.broadcast_tensors(fb, mu)
+        out["umu0"] = torch.where(fb > 0.0, torch.clamp(mu, min=umu0_min), mu)
+    return out
+
+
+def _beam_hint(bc) -> str:
+    """After a failed synchronous call: name the beam inputs cdisort's c_chekin rejects."""
+    try:
+        if not bc or bc.get("fbeam") is None or bc.get("umu0") is None:
+            return ""
+        fb, mu = torch.broadcast_tensors(torch.as_tensor(bc["fbeam"]), torch.as_tensor(bc["umu0"]))
+        bad = int(((fb > 0.0) & ~((mu > 0.0) & (mu <= 1.0))).sum())
+    except Exception:  # the hint must never mask the original error
+        return ""
+    if not bad:
+        return ""
+    return (f" -- {bad} solve(s) have fbeam > 0 with umu0 outside (0, 1], which cdisort's "
+            "c_chekin rejects; for a day/night batch use "
+            "pyharp_amd.night_side_beam(bc, mode='dark' or 'clamp')")
+
+
 class _DisortState:
     """Subset of cdisort's disort_state exposed by ``DisortOptions.ds()``."""
 
@@ -229,7 +278,12 @@ class Disort(RTSolver):
     def forward(self, prop: torch.Tensor, bc: Optional[Dict[str, torch.Tensor]] = None,
                 temf: Optional[torch.Tensor] = None, *, status: Optional[torch.Tensor] = None,
                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        return self._forward(prop, bc, temf, status=status, out=out)
+        try:
+            return self._forward(prop, bc, temf, status=status, out=out)
+        except RuntimeError as err:
+            if "at least one solve failed" in str(err) and _beam_hint(bc):
+                raise RuntimeError(str(err) + _beam_hint(bc)) from err
+            raise
 
     def forward_band(self, prop: torch.Tensor, bc: Optional[Dict[str, torch.Tensor]] = None,
                      temf: Optional[torch.Tensor] = None, *, weights: torch.Tensor,
@@ -244,7 +298,12 @@ class Disort(RTSolver):
         if self.radiance:
             raise RuntimeError("Disort.forward_band: the fused band sum is a flux-only path "
                                "(onlyfl without usrtau)")
-        return self._forward(prop, bc, temf, status=status, out=flux, band=(weights, out))
+        try:
+            return self._forward(prop, bc, temf, status=status, out=flux, band=(weights, out))
+        except RuntimeError as err:
+            if "at least one solve failed" in str(err) and _beam_hint(bc):
+                raise RuntimeError(str(err) + _beam_hint(bc)) from err
+            raise
 
     def _forward(self, prop, bc, temf, *, status=None, out=None, band=None):
         op = self.options

@@ -1,5 +1,6 @@
 #!/bin/bash
 # A/B: bench.py (C4, no CPU baseline) for each library variant given as mb/<name>/libhdisort.so ("cur" = in-tree)
+export HD_AB=1  # the A/B switches below are read only with this opt-in
 set -e -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/ab

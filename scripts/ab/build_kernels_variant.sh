@@ -2,6 +2,7 @@
 # build_kernels_variant.sh NAME SED_EXPR : libhdisort with one sed edit applied to hd_kernels.hip only
 # -> mb/NAME/libhdisort.so (the other translation units are compiled once into mb/_objs and reused).
 # A/B runs load it via HD_LIB_PATH (scripts/ab/ab.sh).
+export HD_AB=1  # the A/B switches below are read only with this opt-in
 set -e
 NAME=$1; EXPR=$2
 R=/root/repo; C=$R/pyharp_amd/csrc; O=$R/mb/_objs

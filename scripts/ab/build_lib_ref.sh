@@ -1,6 +1,7 @@
 #!/bin/bash
 # build_lib_ref.sh NAME GITREF : libhdisort from the sources of commit GITREF -> mb/NAME/libhdisort.so
 # (A/B of the working tree against a commit, loaded via HD_LIB_PATH)
+export HD_AB=1  # the A/B switches below are read only with this opt-in
 set -e
 NAME=$1; REF=$2
 D=/root/repo/mb/$NAME

@@ -1,6 +1,7 @@
 #!/bin/bash
 # build_lib_rev.sh NAME REV : libhdisort built from the sources of git revision REV
 # -> mb/NAME/libhdisort.so (A/B runs via HD_LIB_PATH, e.g. scripts/ab/c4_ab.sh)
+export HD_AB=1  # the A/B switches below are read only with this opt-in
 set -e
 NAME=$1; REV=$2
 D=/root/repo/mb/$NAME

@@ -1,6 +1,7 @@
 #!/bin/bash
 # build_lib_variant.sh NAME SED_EXPR FILE : libhdisort built from the in-tree sources with one
 # sed edit applied to pyharp_amd/csrc/FILE -> mb/NAME/libhdisort.so (A/B runs via HD_LIB_PATH)
+export HD_AB=1  # the A/B switches below are read only with this opt-in
 set -e
 NAME=$1; EXPR=$2; FILE=$3
 D=/root/repo/mb/$NAME

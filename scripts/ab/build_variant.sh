@@ -2,6 +2,7 @@
 # Build libhdisort.so with extra compile flags into ab_libs/libhdisort_NAME.so (for
 # A/B runs on one box: HD_LIB_PATH=ab_libs/libhdisort_NAME.so python ...):
 #   bash scripts/ab/build_variant.sh NAME -DFLAG=VALUE ...
+export HD_AB=1  # the A/B switches below are read only with this opt-in
 set -e
 NAME=$1; shift
 OUT=ab_libs/obj_$NAME; mkdir -p $OUT

@@ -2,6 +2,7 @@
 # C4 / 8-GPU-rank-shape A/B of library variants (mb/<name>/libhdisort.so; "cur" = in-tree),
 # after the register-path parity tests on the in-tree library:
 #   gpurun -- bash scripts/ab/c4_ab.sh TAG cur v1 cur v1 ...
+export HD_AB=1  # the A/B switches below are read only with this opt-in
 set -e -o pipefail
 TAG=$1; shift
 OUT=gpurun_out/$TAG; mkdir -p $OUT

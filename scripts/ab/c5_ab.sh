@@ -2,6 +2,7 @@
 # C5 A/B of library variants (mb/<name>/libhdisort.so; "cur" = in-tree): team parity
 # tests on each, then the C5 bench with the CPU-restatement comparison (max_rel_err).
 #   gpurun -- bash scripts/ab/c5_ab.sh TAG cur v1 v2 ...
+export HD_AB=1  # the A/B switches below are read only with this opt-in
 set -e -o pipefail
 TAG=$1; shift
 OUT=gpurun_out/$TAG; mkdir -p $OUT

@@ -2,6 +2,7 @@
 # A/B of an environment switch on the in-tree library: register-path parity tests
 # with the switch at its first value, then C4 and the 8-GPU rank shape for each value.
 #   gpurun -- bash scripts/ab/env_ab.sh TAG VAR v1 v2 [v1 v2 ...]
+export HD_AB=1  # the A/B switches below are read only with this opt-in
 set -e -o pipefail
 TAG=$1; VAR=$2; shift 2
 OUT=gpurun_out/$TAG; mkdir -p $OUT

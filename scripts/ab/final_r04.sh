@@ -2,6 +2,7 @@
 # End-of-round verification on one box: every GPU test, the smoke, the driver's bench
 # line, C5 / C1 lines, radiance throughput at nstr 32 / 24 / 16 and a kernel-stats
 # profile of the nstr-32 radiance run.  gpurun -- bash scripts/ab/final_r04.sh TAG
+export HD_AB=1  # the A/B switches below are read only with this opt-in
 set -e -o pipefail
 TAG=$1
 bash scripts/gpu.sh $TAG tests smoke bench=c4 "bench=c5:--config,c5,--steps,10,--warmup,3,--no-extra" \

@@ -3,6 +3,7 @@
 # one-wave sweep.  Team-path parity tests with the lean sweep, the bitwise test,
 # then C5 / C5s alternating the two (same box), and a C5 timeline with the lean sweep:
 #   gpurun -- bash scripts/ab/lean_ab.sh TAG [ROUNDS]
+export HD_AB=1  # the A/B switches below are read only with this opt-in
 set -e -o pipefail
 TAG=$1; ROUNDS=${2:-2}
 OUT=gpurun_out/$TAG; mkdir -p $OUT

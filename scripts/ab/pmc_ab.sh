@@ -1,5 +1,6 @@
 #!/bin/bash
 # SQ stall counters + I-cache counters for library variants mb/<name> (one C4 chunk)
+export HD_AB=1  # the A/B switches below are read only with this opt-in
 set -e -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/pmcab; mkdir -p $OUT

@@ -3,6 +3,7 @@
 # one-lane sweep.  The register-path GPU tests with the team sweep, then C1 / C3 /
 # C3l alternating the two (same box), and a C3l timeline with the team sweep:
 #   gpurun -- bash scripts/ab/quad_ab.sh TAG [ROUNDS]
+export HD_AB=1  # the A/B switches below are read only with this opt-in
 set -e -o pipefail
 TAG=$1; ROUNDS=${2:-2}
 OUT=gpurun_out/$TAG; mkdir -p $OUT

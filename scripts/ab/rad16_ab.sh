@@ -1,6 +1,7 @@
 #!/bin/bash
 # nstr-16 radiance: default library against ab_libs variants (HD_LIB_PATH), alternating
 #   gpurun -- bash scripts/ab/rad16_ab.sh TAG VARIANT...
+export HD_AB=1  # the A/B switches below are read only with this opt-in
 set -e -o pipefail
 TAG=$1; shift
 OUT=gpurun_out/$TAG; mkdir -p $OUT

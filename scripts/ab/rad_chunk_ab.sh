@@ -1,6 +1,7 @@
 #!/bin/bash
 # radiance throughput against the chunk size (solves per chunk): scripts/bench_rad.py
 #   gpurun -- bash scripts/ab/rad_chunk_ab.sh TAG
+export HD_AB=1  # the A/B switches below are read only with this opt-in
 set -e -o pipefail
 TAG=$1
 OUT=gpurun_out/$TAG; mkdir -p $OUT

@@ -1,6 +1,7 @@
 #!/bin/bash
 # SQ / TCC counters of the intensity-path kernels (scripts/bench_rad.py, small shape),
 # one --pmc pass per counter group:  gpurun -- bash scripts/ab/rad_pmc.sh TAG NSTR
+export HD_AB=1  # the A/B switches below are read only with this opt-in
 set -e -o pipefail
 TAG=$1; N=${2:-16}
 OUT=gpurun_out/$TAG; mkdir -p $OUT

@@ -3,6 +3,7 @@
 # (HD_RAD_USER=rolled).  Radiance GPU tests, then scripts/bench_rad.py A/B and a
 # kernel-stats profile of the team version:
 #   gpurun -- bash scripts/ab/rad_user_ab.sh TAG
+export HD_AB=1  # the A/B switches below are read only with this opt-in
 set -e -o pipefail
 TAG=$1
 OUT=gpurun_out/$TAG; mkdir -p $OUT

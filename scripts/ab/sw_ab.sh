@@ -1,3 +1,4 @@
+export HD_AB=1  # the A/B switches below are read only with this opt-in
 set -e -o pipefail
 OUT=gpurun_out/r2s3_swab; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"

@@ -3,6 +3,7 @@
 # Jacobi sweep counts at nstr 32, then C5 (with the CPU-restatement deviation on the
 # bench sample) for the in-tree library and a baseline variant, alternating.
 #   gpurun -- bash scripts/ab/team_ab.sh TAG BASE
+export HD_AB=1  # the A/B switches below are read only with this opt-in
 set -e -o pipefail
 TAG=$1; BASE=$2
 OUT=gpurun_out/$TAG; mkdir -p $OUT

@@ -3,6 +3,7 @@
 # baseline variant: register + team parity tests on the in-tree library, then C4,
 # the 8-GPU rank shape and C5, alternating.
 #   gpurun -- bash scripts/ab/warm_ab.sh TAG BASE
+export HD_AB=1  # the A/B switches below are read only with this opt-in
 set -e -o pipefail
 TAG=$1; BASE=$2
 OUT=gpurun_out/$TAG; mkdir -p $OUT

@@ -62,3 +62,39 @@ def test_spawn_ranks_reports_a_failed_rank(tmp_path):
     prog = [sys.executable, "-c", _RANK_PROG, str(tmp_path)]
     env = dict(os.environ, FAIL_RANK="1")
     assert bench.spawn_ranks(2, [], env=env, program=prog) == 3
+
+
+_PARENT_PROG = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import bench
+child = [sys.executable, "-c",
+         "import os, sys, time; open(os.path.join(sys.argv[1], 'pid' + os.environ['RANK']), 'w')"
+         ".write(str(os.getpid())); time.sleep(600)", sys.argv[2]]
+sys.exit(bench.spawn_ranks(2, [], program=child))
+"""
+
+
+def test_spawn_ranks_terminated_parent_stops_its_ranks(tmp_path):
+    """A SIGTERM to the spawning parent (a driver timeout) ends its ranks too: none
+    keeps holding a GPU or waits in a collective after the parent is gone."""
+    import signal
+    import time
+    parent = subprocess.Popen([sys.executable, "-c", _PARENT_PROG, ROOT, str(tmp_path)])
+    pids = []
+    deadline = time.time() + 120
+    while time.time() < deadline and len(pids) < 2:
+        pids = [int(p.read_text()) for p in tmp_path.glob("pid*") if p.read_text()]
+        time.sleep(0.1)
+    assert len(pids) == 2
+    parent.send_signal(signal.SIGTERM)
+    assert parent.wait(timeout=60) == 128 + signal.SIGTERM
+    for pid in pids:
+        for _ in range(100):
+            try:
+                os.kill(pid, 0)
+            except ProcessLookupError:
+                break
+            time.sleep(0.1)
+        else:
+            raise AssertionError(f"rank {pid} outlived its parent")

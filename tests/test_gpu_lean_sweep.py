@@ -43,9 +43,9 @@ def _solve(nstr, planck, chunk=23):
 @pytest.mark.parametrize("nstr,planck", [(18, False), (24, True), (32, False), (32, True)])
 def test_lean_sweep_bitwise(nstr, planck, tmp_path):
     here = _solve(nstr, planck)
-    lean_here = os.environ.get("HD_TEAM_SWEEP_LEAN", "1") != "0"
+    lean_here = not (os.environ.get("HD_AB") == "1" and os.environ.get("HD_TEAM_SWEEP_LEAN") == "0")
     out = tmp_path / "other.npy"
-    env = dict(os.environ, HD_TEAM_SWEEP_LEAN="0" if lean_here else "1")
+    env = dict(os.environ, HD_AB="1", HD_TEAM_SWEEP_LEAN="0" if lean_here else "1")
     subprocess.run([sys.executable, "-c", CHILD, ROOT, str(nstr), "1" if planck else "0",
                     str(out)], check=True, env=env, timeout=300)
     other = np.load(out)

@@ -574,6 +574,31 @@ def test_umu0_as_given(oracle_c, nstr):
         assert np.all(np.isfinite(g))
 
 
+@pytest.mark.parametrize("nstr", [16, 32])
+def test_day_night_batch(oracle_c, nstr):
+    """A GCM-style batch -- one fbeam, cos(zenith) over day and night side -- fails
+    with a message that names the night-side solves and the helper; with
+    pyharp_amd.night_side_beam(bc, 'dark') the night side has no direct beam and every
+    solve matches the C oracle run on the same converted inputs (register nstr 16 and
+    team nstr 32 paths)."""
+    from pyharp_amd import night_side_beam
+    rng = np.random.default_rng(777 + nstr)
+    nwave, ncol, nlyr = 2, 12, 16
+    prop, bc, _ = _random_batch(rng, nwave, ncol, nlyr, nstr, False)
+    bc["fbeam"] = np.ones((nwave, ncol))
+    bc["umu0"] = np.broadcast_to(np.cos(np.linspace(0.1, 3.0, ncol)), (nwave, ncol)).copy()
+    d = _disort(nstr, nlyr, nwave, ncol)
+    with pytest.raises(RuntimeError, match=r"umu0 outside \(0, 1\].*night_side_beam"):
+        _run(d, prop, bc)
+    bcd = {k: np.asarray(v) for k, v in
+           night_side_beam({k: torch.as_tensor(v) for k, v in bc.items()}, "dark").items()}
+    assert np.all(bcd["fbeam"][bc["umu0"] <= 0.0] == 0.0)
+    f = _run(d, prop, bcd)
+    ref = oracle_c.forward(prop, bcd, nstr=nstr)
+    err = rel_err(f, ref).max()
+    assert margin(err) < TOL, f"nstr={nstr}: max rel err {err:.3e}"
+
+
 @pytest.mark.parametrize("nstr", [8, 32])
 def test_eigen_status_when_jacobi_capped(nstr):
     """A Jacobi still rotating at the sweep cap is reported (HD_STATUS_EIGEN, an

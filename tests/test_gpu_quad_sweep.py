@@ -43,9 +43,9 @@ def _solve(nstr, planck, chunk=23):
 @pytest.mark.parametrize("nstr,planck", [(4, False), (4, True), (8, False), (8, True)])
 def test_quad_sweep_matches_one_lane(nstr, planck, tmp_path):
     here = _solve(nstr, planck)
-    quad_here = os.environ.get("HD_SWEEP_QUAD", "-1") != "0"
+    quad_here = not (os.environ.get("HD_AB") == "1" and os.environ.get("HD_SWEEP_QUAD") == "0")
     out = tmp_path / "other.npy"
-    env = dict(os.environ, HD_SWEEP_QUAD="0" if quad_here else "1")
+    env = dict(os.environ, HD_AB="1", HD_SWEEP_QUAD="0" if quad_here else "1")
     subprocess.run([sys.executable, "-c", CHILD, ROOT, str(nstr), "1" if planck else "0",
                     str(out)], check=True, env=env, timeout=300)
     other = np.load(out)

@@ -383,7 +383,7 @@ def test_team_user_kernel_matches_rolled(nstr, planck, usrtau, nwave, tmp_path):
     here = _user_case(nstr, planck, usrtau, nwave)
     out = tmp_path / "rolled.npy"
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, HD_RAD_USER="rolled")
+    env = dict(os.environ, HD_AB="1", HD_RAD_USER="rolled")
     subprocess.run([sys.executable, "-c", _USER_CHILD, root, str(nstr), "1" if planck else "0",
                     "1" if usrtau else "0", str(out), str(nwave)], check=True, env=env,
                    timeout=300)

@@ -49,10 +49,10 @@ def _solve(nstr, prop, bc):
 
 @pytest.mark.parametrize("nstr", [20, 32])
 def test_warm_start_matches_cold_start(nstr, tmp_path):
-    assert os.environ.get("HD_JACOBI_WARM", "1") != "0"
+    assert not (os.environ.get("HD_AB") == "1" and os.environ.get("HD_JACOBI_WARM") == "0")
     warm = _solve(nstr, *_batch(nstr))
     out = tmp_path / "cold.npy"
-    env = dict(os.environ, HD_JACOBI_WARM="0")
+    env = dict(os.environ, HD_AB="1", HD_JACOBI_WARM="0")
     subprocess.run([sys.executable, "-c", CHILD, ROOT, str(nstr), str(out)], check=True,
                    env=env, timeout=300)
     cold = np.load(out)

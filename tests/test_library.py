@@ -173,6 +173,11 @@ def test_cpp_flag_semantics():
     exe = os.path.join(os.path.dirname(__file__), "cpp", "flags_check")
     src = exe + ".cpp"
     hdr = os.path.join(os.path.dirname(__file__), "..", "include", "harp_amd", "disort.hpp")
+    lib = os.path.join(os.path.dirname(__file__), "..", "pyharp_amd", "libhdisort.so")
+    if not os.path.exists(lib):
+        pytest.skip("libhdisort.so is not built (python -c 'import __graft_entry__ as g; g.build()')")
+    if not os.path.exists(exe) and not os.path.exists("/opt/rocm/bin/hipcc"):
+        pytest.skip("no hipcc to build tests/cpp/flags_check")
     if not os.path.exists(exe) or os.path.getmtime(exe) < max(os.path.getmtime(src),
                                                               os.path.getmtime(hdr)):
         torch_dir = os.path.dirname(torch.__file__)
@@ -263,3 +268,41 @@ def test_scattering_moments():
     assert r[1] == 0.1 and r.abs().sum() == 0.1
     h = scattering_moments(4, PhaseMomentOptions().type(kHenyeyGreenstein).gg(0.5))
     assert torch.allclose(h, torch.tensor([0.5, 0.25, 0.125, 0.0625], dtype=torch.float64))
+
+
+def test_night_side_beam():
+    """pyharp_amd.night_side_beam: 'dark' switches the beam off where umu0 <= 0,
+    'clamp' floors umu0 at 1e-3 where fbeam > 0 (harp's legacy convention); the
+    caller's tensors are left alone and umu0 > 1 is not hidden."""
+    from pyharp_amd import night_side_beam
+    fb = torch.ones(2, 3)
+    mu = torch.tensor([[0.5, -0.1, 0.0], [1.0, 0.2, 1.5]])
+    d = night_side_beam({"fbeam": fb, "umu0": mu, "albedo": 0.3 * fb}, "dark")
+    assert torch.equal(d["fbeam"], torch.tensor([[1.0, 0.0, 0.0], [1.0, 1.0, 1.0]]))
+    assert d["umu0"] is mu and torch.equal(fb, torch.ones(2, 3))
+    c = night_side_beam({"fbeam": torch.tensor([[1.0, 1.0, 0.0], [1.0, 1.0, 1.0]]), "umu0": mu},
+                        "clamp")
+    assert torch.equal(c["umu0"], torch.tensor([[0.5, 1e-3, 0.0], [1.0, 0.2, 1.5]]))
+    assert night_side_beam({"albedo": fb}) == {"albedo": fb}
+    with pytest.raises(ValueError):
+        night_side_beam({"fbeam": fb, "umu0": mu}, "floor")
+
+
+def test_chunk_plan(lib):
+    """The automatic chunking (hd_chunk_solves; no device needed).  Register path
+    (nstr <= 16): ~65 536 solves per chunk, one sweep wave per SIMD -- C4 640 000 solves
+    in 10 chunks, the 8-GPU rank shape 80 000 in 2.  Team path (nstr 18..32): a 16 GB
+    scratch budget bounds the chunk (C5 64 000 solves: 4 chunks of 16 000), and a call
+    that fits one chunk still takes two from 4 096 solves up, so the second chunk's
+    layer kernel runs beside the first one's sweep (the 8-GPU C5 rank shape, 8 g-points
+    x 1 000 columns: 2 x 4 000)."""
+    from pyharp_amd import _lib
+    assert _lib.chunk_solves(16, 80, 640000) == 64000
+    assert _lib.chunk_solves(16, 80, 80000) == 40000
+    assert _lib.chunk_solves(16, 80, 16) == 16
+    assert _lib.chunk_solves(32, 80, 64000) == 16000
+    assert _lib.chunk_solves(32, 80, 8000) == 4000
+    assert _lib.chunk_solves(32, 80, 4095) == 4095
+    assert _lib.chunk_solves(32, 80, 4097) == 2049
+    with pytest.raises(RuntimeError):
+        _lib.chunk_solves(15, 80, 100)
