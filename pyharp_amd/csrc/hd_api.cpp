@@ -213,10 +213,6 @@ int ensure_rad_tables(hd_context* ctx) {
   return HD_OK;
 }
 
-// team path: below this many solves per chunk a chunk's sweep (16 lanes per solve)
-// no longer fills the SIMDs it could share with the next chunk's layer kernel
-constexpr long kTeamMinChunk = 2048;
-
 long auto_chunk(long nsolve, int nn, int nlyr, bool planck) {
   // NN <= 8: the sweep runs one lane per solve at one wave per SIMD (its
   // register file is full), so a chunk of 65 536 solves is one wave on each of
@@ -232,13 +228,11 @@ long auto_chunk(long nsolve, int nn, int nlyr, bool planck) {
     const double per = 8.0 * (double)hd::scratch_doubles_per_solve(nn, nlyr, planck);
     target = std::min<long>(262144, std::max<long>(16384, (long)(budget / per)));
   }
-  if (nsolve <= target) {
-    // team path: a call that fits one chunk still takes two, so the second chunk's
-    // layer kernel runs beside the first one's sweep (the 8-GPU C5 rank shape is
-    // 8 000 solves: one chunk left the sweep wholly exposed)
-    if (nn > hd::kMaxRegNN && nsolve >= 2 * kTeamMinChunk) return (nsolve + 1) / 2;
-    return nsolve;
-  }
+  // (team path: a call that fits one chunk stays one chunk.  Split in two, the 8-GPU
+  // C5 rank shape -- 8 000 solves -- ran 1.155 M solves/s against 1.268 M: a 4 000-solve
+  // layer kernel takes 2.57 ms alone and 3.63 ms beside the first chunk's sweep,
+  // against 4.59 ms for all 8 000, profiles/r05/c5_rank_shape.txt)
+  if (nsolve <= target) return nsolve;
   const long n = (nsolve + target - 1) / target;
   return (nsolve + n - 1) / n;
 }

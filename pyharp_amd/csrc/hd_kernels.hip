@@ -1534,7 +1534,7 @@ __global__ __launch_bounds__(64) void hd_backsub_tail_kernel(SweepArgs A) {
 // direction): bflux[c] = (first chunk of c ? 0 : bflux[c]) + the chunk's part,
 // summed in wave-point order -- deterministic, no atomics
 // ============================================================================
-__global__ __launch_bounds__(256) void hd_band_reduce_kernel(BandArgs B) {
+__global__ __launch_bounds__(64) void hd_band_reduce_kernel(BandArgs B) {
   const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int per = 2 * B.nlev;
   const long W = B.nwave;
@@ -1576,7 +1576,9 @@ hipError_t launch_band_reduce(const BandArgs& ba, hipStream_t stream) {
   } else {
     n = (long)ba.ncol * 2 * ba.nlev;
   }
-  hipLaunchKernelGGL(hd_band_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+  // one-wave blocks: on the side stream beside a team layer kernel (two 239-VGPR waves
+  // per SIMD) a 4-wave block waited up to 9 ms for a CU with four free wave slots
+  hipLaunchKernelGGL(hd_band_reduce_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0,
                      stream, ba);
   return hipGetLastError();
 }

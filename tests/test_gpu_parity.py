@@ -174,6 +174,41 @@ def test_bench_c5_workload_slab(oracle_c):
     assert margin(err) < TOL, f"max rel err {err:.3e}"
 
 
+def test_bench_c5_rank_shape_band(oracle_c):
+    """The 8-GPU C5 rank shape as ``bench.py --config c5 --gpus 8`` gives rank 0: the
+    g-points {0, 8, ..., 56} x 1000 columns (8 000 solves), through the fused band
+    path, one chunk as the automatic plan runs it and two (the side-stream band
+    reduce of chunk 0 beside chunk 1's sweep); the band flux of the first 64 columns
+    against the C oracle's weighted sum of per-point fluxes."""
+    import bench
+    from pyharp_amd import _lib
+    dev = torch.device("cuda", 0)
+    gpts = list(range(0, 64, 8))
+    ncol, nlyr, nstr = 1000, 80, 32
+    from pyharp_amd.disort import _context
+    assert _lib.chunk_solves(nstr, nlyr, len(gpts) * ncol) == 8000
+    prop, bc, _ = bench.make_aerosol_inputs(gpts, 64, ncol, nlyr, nstr, dev)
+    d = _disort(nstr, nlyr, len(gpts), ncol)
+    w = torch.linspace(0.5, 1.5, len(gpts), dtype=torch.float64, device=dev) / len(gpts)
+    band = d.forward_band(prop, bc, weights=w).cpu().numpy()
+    ctx = _context(0)
+    ctx.set_chunk(4000)
+    try:
+        band2 = d.forward_band(prop, bc, weights=w).cpu().numpy()
+    finally:
+        ctx.set_chunk(0)
+    # the chunk split changes only the band sum's association order
+    assert np.abs(band2 - band).max() <= 1e-13 * np.abs(band).max()
+    pn = prop.cpu().numpy()
+    bn = {k: v.cpu().numpy() for k, v in bc.items()}
+    ref = np.zeros((len(gpts), ncol, nlyr + 1, 2))
+    for i in range(len(gpts)):
+        oracle_c.forward(pn, bn, nstr=nstr, first=i * ncol, count=64, out=ref)
+    rb = np.einsum("g,gcld->cld", w.cpu().numpy(), ref[:, :64])
+    err = rel_err(band[None, :64], rb[None]).max()
+    assert margin(err) < TOL, f"max rel err {err:.3e}"
+
+
 @pytest.mark.parametrize("nstr,planck", [(8, False), (24, False), (24, True), (32, True)])
 def test_chunking_invariance_team(nstr, planck):
     """Several chunks: the two-stream pipelines (team path: chunk k+1's prologue and

@@ -292,17 +292,16 @@ def test_chunk_plan(lib):
     """The automatic chunking (hd_chunk_solves; no device needed).  Register path
     (nstr <= 16): ~65 536 solves per chunk, one sweep wave per SIMD -- C4 640 000 solves
     in 10 chunks, the 8-GPU rank shape 80 000 in 2.  Team path (nstr 18..32): a 16 GB
-    scratch budget bounds the chunk (C5 64 000 solves: 4 chunks of 16 000), and a call
-    that fits one chunk still takes two from 4 096 solves up, so the second chunk's
-    layer kernel runs beside the first one's sweep (the 8-GPU C5 rank shape, 8 g-points
-    x 1 000 columns: 2 x 4 000)."""
+    scratch budget bounds the chunk (C5 64 000 solves: 4 chunks of 16 000); the 8-GPU
+    C5 rank shape (8 g-points x 1 000 columns) stays one chunk -- split in two it ran
+    9 % slower (profiles/r05/c5_rank_shape.txt)."""
     from pyharp_amd import _lib
     assert _lib.chunk_solves(16, 80, 640000) == 64000
     assert _lib.chunk_solves(16, 80, 80000) == 40000
     assert _lib.chunk_solves(16, 80, 16) == 16
     assert _lib.chunk_solves(32, 80, 64000) == 16000
-    assert _lib.chunk_solves(32, 80, 8000) == 4000
-    assert _lib.chunk_solves(32, 80, 4095) == 4095
-    assert _lib.chunk_solves(32, 80, 4097) == 2049
+    assert _lib.chunk_solves(32, 80, 8000) == 8000
+    assert _lib.chunk_solves(32, 80, 16384) == 16384
+    assert _lib.chunk_solves(32, 80, 16385) == 8193
     with pytest.raises(RuntimeError):
         _lib.chunk_solves(15, 80, 100)
