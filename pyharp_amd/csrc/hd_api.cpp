@@ -53,6 +53,9 @@ struct hd_context {
   // and each runs 1.85 ms against hd_sweep_kernel's 1.4 (C4 12.38 vs 12.77 M,
   // profiles/r05/lean8_ab.txt); HD_AB=1 HD_SWEEP_LEAN8=1 picks it
   int lean8 = 0;
+  // nstr 16: layer setup, adding sweep and back-substitution of a chunk in one kernel
+  // (hd_column_kernel: no layer records in HBM); HD_AB=1 HD_COLUMN=0|1
+  int column = 0;
   // true while a solve enqueues into a capturing stream: scratch may not grow then
   bool capturing = false;
   std::string err;
@@ -402,6 +405,7 @@ int hd_context_create(hd_context** out, int device) {
   if (const char* e = hd::ab_env("HD_TEAM_SWEEP_LEAN")) ctx->lean = std::atoi(e) != 0;
   if (const char* e = hd::ab_env("HD_SWEEP_QUAD")) ctx->quad = std::atoi(e) < 0 ? -1 : std::atoi(e) != 0;
   if (const char* e = hd::ab_env("HD_SWEEP_LEAN8")) ctx->lean8 = std::atoi(e) != 0;
+  if (const char* e = hd::ab_env("HD_COLUMN")) ctx->column = std::atoi(e) != 0;
   ctx->device = device;
   auto init = [ctx]() -> int {
     HD_HIP(ctx, hipSetDevice(ctx->device));
@@ -589,7 +593,9 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
   // a register-path call of one chunk has nothing to overlap: it runs wholly on
   // the caller's stream (prologue, layer kernel, sweep, tail back-substitution),
   // without the fork/join of the three-stream pipeline below (C1/C3 latency)
-  const bool single = reg && nsolve <= chunk;
+  // nstr 16 by the column kernel: every chunk wholly on the caller's stream
+  const bool col = reg && nn == 8 && ctx->column;
+  const bool single = reg && !col && nsolve <= chunk;
   // team path with several chunks: chunk k+1's prologue and layer kernel on the
   // `lay` stream beside chunk k's sweep on the caller's stream
   const bool team_pipe = !reg && nsolve > chunk;
@@ -686,7 +692,7 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
     pa.nwave = in->nwave;
   };
 
-  if ((reg && !single) || team_pipe) {
+  if ((reg && !single && !col) || team_pipe) {
     // fork: the side stream sees everything the caller's stream did before this
     // call (the inputs) -- and, under stream capture, joins the graph here
     HD_HIP(ctx, hipEventRecord(ctx->ev_fork, stream));
@@ -704,7 +710,7 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
       // buffer `buf` is free once sweep k-2 (its last reader) is done
       if (k >= 2) HD_HIP(ctx, hipStreamWaitEvent(ctx->lay, ctx->ev_sweep[buf], 0));
       hd::launch_prologue(planck ? &pa : nullptr, need_tauc ? &ta : nullptr, ctx->lay);
-    } else if (!reg || single) {
+    } else if (!reg || single || col) {
       hd::launch_prologue(planck ? &pa : nullptr, need_tauc ? &ta : nullptr, stream);
     } else if (k == 0 && need_pro) {
       hd::launch_prologue(planck ? &pa : nullptr, need_tauc ? &ta : nullptr, ctx->side);
@@ -780,7 +786,14 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
       ctx->pool_used += 4;
     }
     hipError_t e = hipSuccess;
-    if (single) {
+    if (col) {
+      if (ev) HD_HIP(ctx, hipEventRecord(ev[0], stream));
+      e = hd::launch_column_nn(nn, la, sa, stream);
+      if (ev) HD_HIP(ctx, hipEventRecord(ev[1], stream));
+      if (ev) HD_HIP(ctx, hipEventRecord(ev[2], stream));
+      if (ev) HD_HIP(ctx, hipEventRecord(ev[3], stream));
+      if (e == hipSuccess && band) e = hd::launch_band_reduce(band_args(s0, nsc, buf), stream);
+    } else if (single) {
       if (ev) HD_HIP(ctx, hipEventRecord(ev[0], stream));
       e = hd::launch_layer_nn(nn, la, stream);
       if (ev) HD_HIP(ctx, hipEventRecord(ev[1], stream));
@@ -835,7 +848,7 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
       if (e == hipSuccess && band) e = hd::launch_band_reduce(band_args(s0, nsc, buf), stream);
     }
     if (e != hipSuccess) return fail(ctx, HD_EHIP, "hd_solve: launch failed: %s", hipGetErrorString(e));
-    if (reg && !single) {
+    if (reg && !single && !col) {
       HD_HIP(ctx, hipEventRecord(ctx->ev_sweep[buf], stream));
       // next chunk's prologue into the other buffer (free: the side stream already
       // waited for the sweep of chunk k-1, the last user of that buffer)
@@ -864,7 +877,7 @@ int solve_enqueue(hd_context* ctx, const hd_config* cfg, const hd_inputs* in, do
       HD_HIP(ctx, hipEventRecord(ctx->ev_back[buf], ctx->side));
     }
   }
-  if ((reg && !single) || (team_pipe && band)) {  // every chunk's fluxes complete
+  if ((reg && !single && !col) || (team_pipe && band)) {  // every chunk's fluxes complete
     for (long b = 0; b < std::min<long>(k, 2); ++b)
       HD_HIP(ctx, hipStreamWaitEvent(stream, ctx->ev_back[b], 0));
   }

@@ -60,6 +60,16 @@ __device__ __forceinline__ const Quad<NN>& quad() {
   else if constexpr (NN == 7) return c_quad.q7;
   else return c_quad.q8;
 }
+// the same table through a pointer the compiler cannot see through: inside a
+// loop, products of table entries are then formed where used instead of being
+// hoisted out of the loop and held (the column kernel's layer loop spilled 60 of
+// them), and the entries come back by scalar loads
+template <int NN>
+__device__ __forceinline__ const Quad<NN>& quad_opaque() {
+  const Quad<NN>* p = &quad<NN>();
+  asm volatile("" : "+s"(p));
+  return *p;
+}
 
 // one wave per block: a layer-kernel wave can take any SIMD the previous chunk's
 // sweep leaves free (hd_solve runs the two on separate streams)
@@ -117,34 +127,51 @@ __global__ __launch_bounds__(256) void hd_tauc_kernel(TaucArgs A) {
 // ============================================================================
 // K1: per-(solve, layer) setup
 // ============================================================================
+// Psi^T staging per lane; also holds L while the Jacobi runs (NN = 2: 5 > 4 doubles)
 template <int NN>
-__global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
-  constexpr int N = 2 * NN;
-  // Psi^T staging; also holds L while the Jacobi runs (NN = 2: 5 > 4 doubles)
-  constexpr int kPsi = NN > 1 ? (NN == 2 ? 5 : NN * NN) : 1;
-  __shared__ double psi_lds[kPsi * kLayerBlock];  // Psi^T staged per lane
-  const Quad<NN>& Qc = quad<NN>();
-  // block = 64 consecutive solves (one wave each) x kLayersPerBlock consecutive
-  // layers: a wave's stores are coalesced (same layer, consecutive solves).
-  // Neighbouring layers of a solve share 128-B lines of prop (18 doubles per
-  // record), so the blocks of one solve tile are numbered layer-fastest and
-  // dealt to the same XCD (blocks b and b + 8 share an XCD's L2): the second
-  // reader of a line finds it in L2 instead of HBM
-  const int lt = threadIdx.x;
-  const int ntl = (A.nlyr + kLayersPerBlock - 1) / kLayersPerBlock;
-  int ts, tl;
-  {
-    const int nb = (int)gridDim.x, b = (int)blockIdx.x;
-    const int x = b & 7, base = nb >> 3, extra = nb & 7;
-    const int logical = x * base + (x < extra ? x : extra) + (b >> 3);
-    ts = logical / ntl;
-    tl = logical - ts * ntl;
+__host__ __device__ constexpr int psi_doubles() {
+  return NN > 1 ? (NN == 2 ? 5 : NN * NN) : 1;
+}
+
+// On-chip layer record of the column kernel: its layer setup writes the RecL
+// elements here and its adding sweep reads them back -- no record in HBM.  R~ and
+// S~+ (used first) stay in registers (compile-time indices after unrolling); T~,
+// S~- and tau' (used after the sweep's LU) go to this lane's Psi^T staging area
+// of LDS, free between the layer setup's last Psi^T read and the next layer's
+// Jacobi, so that they are not live in registers across the LU.
+template <int NN>
+struct ColRec {
+  using RL = RecL<NN>;
+  static constexpr int kSm = even_up(RL::nsym);  // LDS slot of S~-[0]
+  static_assert(kSm + (RL::Tau + 1 - RL::Sm) <= psi_doubles<NN>() || NN == 1,
+                "T~, S~-, tau' do not fit the Psi^T staging area");
+  double v[RL::T + even_up(NN)];  // R~ | S~+ (at RL::T ..)
+  double* lds;                   // psi_lds + lane
+  __device__ __forceinline__ int slot(int e) const { return e < RL::Sp ? e - RL::T : kSm + (e - RL::Sm); }
+  __device__ __forceinline__ void put(int e, double x) {
+    if (e < RL::T) v[e] = x;
+    else if (e >= RL::Sp && e < RL::Sm) v[RL::T + (e - RL::Sp)] = x;
+    else if (e <= RL::Tau) lds[slot(e) * kLayerBlock] = x;
   }
-  const int sl = ts * 64 + (lt & 63);
-  const int lc = tl * kLayersPerBlock + (lt >> 6);  // solver layer, 0 = top
+  __device__ __forceinline__ double get(int e) const {
+    if (e < RL::T) return v[e];
+    if (e >= RL::Sp && e < RL::Sm) return v[RL::T + (e - RL::Sp)];
+    return lds[slot(e) * kLayerBlock];
+  }
+  __device__ __forceinline__ void close(int) {}
+};
+
+// The layer setup of (solve s, solver layer lc) into the record sink `out`
+// (PairOut: RecL in HBM; RegRec: registers).  psi_lds: this wave's Psi^T
+// staging, element e of lane lt at e * kLayerBlock + lt.  Returns the status bits.
+// OPQ: the quadrature table through quad_opaque (the column kernel's layer loop)
+template <int NN, bool OPQ, class Out>
+__device__ __forceinline__ int layer_body(const LayerArgs& A, long s, int sl, int lc,
+                                          double* psi_lds, int lt, Out& out) {
+  constexpr int N = 2 * NN;
+  constexpr int kPsi = psi_doubles<NN>();
+  const Quad<NN>& Qc = OPQ ? quad_opaque<NN>() : quad<NN>();
   const int L = A.nlyr;
-  if (sl >= A.nsc || lc >= L) return;
-  const long s = solve_of(A.s0 + sl, A.cmaj, A.nwave, A.ncol);
   const int nm = A.nmom;
   const int np = A.nprop;
   int st = 0;
@@ -430,8 +457,6 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
     for (int j = 0; j < NN; ++j) v[i][j] *= dsq[j];
 
   using RL = RecL<NN>;
-  PairOut out{reinterpret_cast<double2*>(A.scr) + (size_t)lc * RL::pairs * A.nsc + sl,
-              (size_t)A.nsc, 0.0};
   constexpr int nsym = NN * (NN + 1) / 2;
   double ga[NN], gb[NN];
 #pragma unroll
@@ -535,6 +560,35 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
   // running product instead of an exp of the running depth
   out.put(RL::Tau + 1, beam ? e0 : 1.0);
   if (!isfinite(chk + taup)) st |= kStNonFinite;
+  return st;
+}
+
+template <int NN>
+__global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
+  __shared__ double psi_lds[psi_doubles<NN>() * kLayerBlock];  // Psi^T staged per lane
+  // block = 64 consecutive solves (one wave each) x kLayersPerBlock consecutive
+  // layers: a wave's stores are coalesced (same layer, consecutive solves).
+  // Neighbouring layers of a solve share 128-B lines of prop (18 doubles per
+  // record), so the blocks of one solve tile are numbered layer-fastest and
+  // dealt to the same XCD (blocks b and b + 8 share an XCD's L2): the second
+  // reader of a line finds it in L2 instead of HBM
+  const int lt = threadIdx.x;
+  const int ntl = (A.nlyr + kLayersPerBlock - 1) / kLayersPerBlock;
+  int ts, tl;
+  {
+    const int nb = (int)gridDim.x, b = (int)blockIdx.x;
+    const int x = b & 7, base = nb >> 3, extra = nb & 7;
+    const int logical = x * base + (x < extra ? x : extra) + (b >> 3);
+    ts = logical / ntl;
+    tl = logical - ts * ntl;
+  }
+  const int sl = ts * 64 + (lt & 63);
+  const int lc = tl * kLayersPerBlock + (lt >> 6);  // solver layer, 0 = top
+  if (sl >= A.nsc || lc >= A.nlyr) return;
+  const long s = solve_of(A.s0 + sl, A.cmaj, A.nwave, A.ncol);
+  PairOut out{reinterpret_cast<double2*>(A.scr) + (size_t)lc * RecL<NN>::pairs * A.nsc + sl,
+              (size_t)A.nsc, 0.0};
+  const int st = layer_body<NN, false>(A, s, sl, lc, psi_lds, lt, out);
   if (st) {
     atomicOr(&A.status[s], st);
     if (st & 0x0F) atomicOr(A.anyerr, 1);
@@ -544,12 +598,14 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
 // ============================================================================
 // K2: per-solve adding sweep + back-substitution
 // ============================================================================
-template <int NN>
-__global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
+// The adding sweep of solve s (chunk lane sl): layer lc's record through
+// rec_at(lc), a callable returning a getter e -> RecL element e (hd_sweep_kernel:
+// loads from the HBM record; hd_column_kernel: the layer setup run right there
+// into registers).  Stores the back-substitution records, the surface level and
+// x; returns the status bits.
+template <int NN, class RecAt>
+__device__ __forceinline__ int sweep_body(const SweepArgs& A, long sl, long s, RecAt&& rec_at) {
   const Quad<NN>& Qc = quad<NN>();
-  const long sl = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (sl >= A.nsc) return;
-  const long s = solve_of(A.s0 + sl, A.cmaj, A.nwave, A.ncol);
   const int L = A.nlyr;
   const size_t nsc = A.nsc;
   constexpr int nsym = NN * (NN + 1) / 2;
@@ -583,8 +639,7 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
   for (int lc = 0; lc < L; ++lc) {
     using RL = RecL<NN>;
     using RB = RecB<NN>;
-    const double2* lp = reinterpret_cast<const double2*>(A.scr) + (size_t)lc * RL::pairs * nsc + sl;
-    auto rec = [&](int e) { return pair_get(lp, nsc, e); };
+    auto rec = rec_at(lc);
     PairOut bp{reinterpret_cast<double2*>(A.bsub) + (size_t)lc * RB::pairs * nsc + sl, nsc, 0.0};
     // this layer's R~ (upper) and S~+ ; each record element is read once
     double rl[NN][NN], spl[NN];
@@ -698,7 +753,10 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
       }
     }
     HD_PHASE();
-    // T~ (upper), read once; ZT = W1^-1 T_l stored column by column
+    // T~ (upper), read once, with S~- and tau': the loads are issued before this
+    // layer's ZT stores and Sd <- T_l u + S- is formed right away.  Loaded after the
+    // stores (where Sd is first needed), each S~- element's s_waitcnt also waited for
+    // all 32 ZT stores to retire -- four round trips per layer
     double tl[NN][NN];
     {
       int e = 0;
@@ -706,6 +764,20 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
       for (int i = 0; i < NN; ++i)
 #pragma unroll
         for (int j = i; j < NN; ++j) tl[i][j] = rec(RL::T + (e++));
+    }
+    {
+      double sm_[NN];
+#pragma unroll
+      for (int i = 0; i < NN; ++i) sm_[i] = rec(RL::Sm + i);
+      const double taul = rec(RL::Tau);
+#pragma unroll
+      for (int i = 0; i < NN; ++i) {
+        double t = sm_[i] * sscale;
+#pragma unroll
+        for (int k = 0; k < NN; ++k) t = fma(HD_SYM(tl, i, k), u[k], t);
+        sd[i] = t;
+      }
+      tauc += taul;
     }
 #pragma unroll
     for (int j = 0; j < NN; ++j) {
@@ -743,7 +815,7 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
       for (int j = 0; j < NN; ++j) am[r][j] = row[j];
     }
     HD_PHASE();
-    // Ra <- R_l + T_l P (upper) ; Sd <- T_l u + S-
+    // Ra <- R_l + T_l P (upper)
 #pragma unroll
     for (int i = 0; i < NN; ++i) {
 #pragma unroll
@@ -753,12 +825,7 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
         for (int k = 0; k < NN; ++k) t = fma(HD_SYM(tl, i, k), am[k][j], t);
         ra[i][j] = t;
       }
-      double t = rec(RL::Sm + i) * sscale;
-#pragma unroll
-      for (int k = 0; k < NN; ++k) t = fma(HD_SYM(tl, i, k), u[k], t);
-      sd[i] = t;
     }
-    tauc += rec(RL::Tau);
   }
 
   // ---- Lambertian surface: I+ = g x ----
@@ -801,10 +868,66 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
   }
   A.xsurf[sl] = x;
   if (!isfinite(chk)) st |= kStNonFinite;
+  return st;
+}
+
+template <int NN>
+__global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
+  const long sl = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (sl >= A.nsc) return;
+  const long s = solve_of(A.s0 + sl, A.cmaj, A.nwave, A.ncol);
+  const size_t nsc = A.nsc;
+  auto rec_at = [&](int lc) {
+    const double2* lp =
+        reinterpret_cast<const double2*>(A.scr) + (size_t)lc * RecL<NN>::pairs * nsc + sl;
+    return [lp, nsc](int e) { return pair_get(lp, nsc, e); };
+  };
+  const int st = sweep_body<NN>(A, sl, s, rec_at);
   if (st) {
     atomicOr(&A.status[s], st);
     if (st & 0x0F) atomicOr(A.anyerr, 1);
   }
+}
+
+template <int NN, bool PRE>
+__device__ __forceinline__ void backsub_body(const SweepArgs& A);
+
+// ============================================================================
+// K1+K2+K3 in one pass per solve (the column kernel): one lane walks its solve's
+// layers top -> bottom, runs each layer's setup (layer_body) into registers and
+// feeds it straight to the adding sweep (sweep_body), then walks back up through
+// the back-substitution records it wrote (backsub_body).  Bitwise the same
+// arithmetic as hd_layer_kernel + hd_sweep_kernel + the back-substitution, but the
+// layer records (RecL: 90 doubles per (solve, layer), written once and read once)
+// never reach HBM, and the three kernels' time-sharing of the SIMDs -- neither
+// the layer kernel nor the sweep leaves room on a SIMD for the other -- becomes
+// one instruction stream per wave.
+// ============================================================================
+template <int NN>
+__global__ __launch_bounds__(64) void hd_column_kernel(LayerArgs LA, SweepArgs A) {
+  __shared__ double psi_lds[psi_doubles<NN>() * kLayerBlock];
+  static_assert(kLayerBlock == 64, "column kernel: one wave per block");
+  const int lt = threadIdx.x;
+  const long sl = (long)blockIdx.x * 64 + lt;
+  if (sl < A.nsc) {
+    const long s = solve_of(A.s0 + sl, A.cmaj, A.nwave, A.ncol);
+    ColRec<NN> r;
+    r.lds = psi_lds + lt;
+    int lst = 0;
+    auto rec_at = [&](int lc) {
+      lst |= layer_body<NN, true>(LA, s, (int)sl, lc, psi_lds, lt, r);
+      return [&r](int e) { return r.get(e); };
+    };
+    const int st = sweep_body<NN>(A, sl, s, rec_at) | lst;
+    if (st) {
+      atomicOr(&A.status[s], st);
+      if (st & 0x0F) atomicOr(A.anyerr, 1);
+    }
+  }
+  // the back-substitution reads what this wave wrote (with the band epilogue, lanes
+  // past the chunk read the last solve's records)
+  __syncthreads();
+  backsub_body<NN, true>(A);
 }
 
 // ============================================================================
@@ -1817,6 +1940,15 @@ hipError_t launch_layer_nn(int nn, const LayerArgs& la, hipStream_t stream) {
   }
   return hipGetLastError();
 }
+hipError_t launch_column_nn(int nn, const LayerArgs& la, const SweepArgs& sa, hipStream_t stream) {
+  const dim3 grid((unsigned)((sa.nsc + 63) / 64)), block(64);
+  switch (nn) {
+    case 8: hipLaunchKernelGGL(hd_column_kernel<8>, grid, block, 0, stream, la, sa); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_sweep_nn(int nn, const SweepArgs& sa, hipStream_t stream) {
   switch (nn) {
     case 1: launch_sweep<1>(sa, stream); break;

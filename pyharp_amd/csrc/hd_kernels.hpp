@@ -238,6 +238,9 @@ hipError_t launch_backsub_nn(int nn, const SweepArgs& sa, hipStream_t stream, bo
 // register path, separately: the layer kernel and the adding sweep of one chunk
 hipError_t launch_layer_nn(int nn, const LayerArgs& la, hipStream_t stream);
 hipError_t launch_sweep_nn(int nn, const SweepArgs& sa, hipStream_t stream);
+// register path, nstr 16: layer setup + adding sweep + back-substitution of one chunk in
+// one kernel (hd_column_kernel; la.scr unused -- no layer records)
+hipError_t launch_column_nn(int nn, const LayerArgs& la, const SweepArgs& sa, hipStream_t stream);
 hipError_t launch_solve_chunk_team(int nn, const PlanckArgs* pa, const TaucArgs* ta,
                                    const LayerArgs& la, const SweepArgs& sa, hipStream_t stream,
                                    hipEvent_t* ev);

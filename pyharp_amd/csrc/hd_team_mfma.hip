@@ -1053,6 +1053,19 @@ __global__ __launch_bounds__(64, 2) void hd_team_mfma_sweep_lean_kernel(SweepArg
       }
       get_m(S1, h, c, li);
       mprod<false>(li, x1, zm, h, c);  // ZT = U^-1 (L^-1 T)
+      // The second reads of T~ and R~ and tau' go out before ZT's stores: a load
+      // issued after a store also waits for that store to retire (one in-order
+      // memory counter), so read after them each waited out 16 store round trips
+      const double taul = rec[2 * NN * NN + 2 * NN];
+      double pm[4][4];
+      mprod<false>(ram, zm, pm, h, c);  // A ZT   (A symmetric: its own transpose)
+      {
+        double tm[4][4];
+        load_m(lc, NN * NN, tm);
+        mprod<false>(tm, pm, ram, h, c);  // T (A ZT)
+      }
+      double rm[4][4];
+      load_m(lc, 0, rm);
 #pragma unroll
       for (int tt = 0; tt < 4; ++tt) {
         double* zr = A.bsub + ((size_t)lc * nsc + (g0 + tt < A.nsc ? g0 + tt : g0)) * ne2t<NN>();
@@ -1064,26 +1077,15 @@ __global__ __launch_bounds__(64, 2) void hd_team_mfma_sweep_lean_kernel(SweepArg
           *((ok && r < NN && c < NN) ? zr + r * NN + c : A.sink + lane) = zm[tt][m];
         }
       }
-      double pm[4][4];
-      mprod<false>(ram, zm, pm, h, c);  // A ZT   (A symmetric: its own transpose)
-      {
-        double tm[4][4];
-        load_m(lc, NN * NN, tm);
-        mprod<false>(tm, pm, ram, h, c);  // T (A ZT)
-      }
-      {
-        double rm[4][4];
-        load_m(lc, 0, rm);
 #pragma unroll
-        for (int tt = 0; tt < 4; ++tt)
+      for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
-          for (int m = 0; m < 4; ++m) ram[tt][m] += rm[tt][m];
-      }
+        for (int m = 0; m < 4; ++m) ram[tt][m] += rm[tt][m];
       lds_fence();
       put_m(S0, h, c, ram);
       lds_fence();
+      tauc += taul;
     }
-    tauc += rec[2 * NN * NN + 2 * NN];
   }
 
   // ---- Lambertian surface: I+ = g x ----
