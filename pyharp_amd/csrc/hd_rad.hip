@@ -887,12 +887,13 @@ template <int NN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HD_RAD_CONST_WAVES)))
 void hd_rad_const_kernel(RadArgs A) {
   const Quad<NN>& Qc = quad_r<NN>();
+  // grid.y = mode (uniform per block: the mode-m tables of the maps are scalar loads)
   const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= (long)A.nu * A.nlyr) return;
-  const int lc = (int)(id / A.nu);
-  const int u = (int)(id - (long)lc * A.nu);
-  const int m = u / A.ns;
-  const int sl = u - m * A.ns;
+  if (id >= (long)A.ns * A.nlyr) return;
+  const int lc = (int)(id / A.ns);
+  const int sl = (int)(id - (long)lc * A.ns);
+  const int m = blockIdx.y;
+  const int u = m * A.ns + sl;
   const long s = A.s0 + sl;
   const size_t nu = A.nu;
   constexpr int nsym = NN * (NN + 1) / 2;
@@ -947,6 +948,98 @@ HD_RUNROLL
     co[j * nu] = cp[j];
     co[(NN + j) * nu] = cm[j];
   }
+#ifndef HD_RAD_WIDE
+  if (A.umap) {
+    // The user-angle integration's angle-independent part, per (unit, layer).  For a
+    // user cosine mu with Y_l^m(mu) = yu_l, split by the parity of l + m into
+    // ye (l = 2 l2 + par) and yo (l = 2 l2 + 1 - par), par = m & 1:
+    //   ce = Me ye,  Me = V^T L^T D Lam_e^T G_e      (the even source projection)
+    //   cx = Mo yo,  Mo = V^T L^-1 D Lam_o^T G_o     (the odd one)
+    //   beam amplitude  ab = abe . ye + abo . yo,  thermal  we = tve . ye, wo = tvo . yo
+    // with D = diag(sqrt(w/mu)), Lam[l][i] = Y_l^m(mu_i), G = diag(gl/2) -- what
+    // hd_rad_user_kernel forms per (unit, angle) from L, V and the moments, regrouped so
+    // that it is formed once per (unit, layer) and each angle pays 2 NN^2 FMAs.
+    // Element e: rsw [layer][e][unit] for e < ne1 (Me row-major, abe, abo, tve), then
+    // bsub [layer][e - ne1][unit] (Mo row-major, tvo).
+    constexpr int N = 2 * NN;
+    constexpr int NE1 = rad_layer_record_doubles(NN);
+    constexpr int NB = rad_bsub_doubles(NN);
+    static_assert(NN * NN + 3 * NN <= NE1 && NN * NN + NN <= NB, "map does not fit");
+    double* m1 = A.rsw + (size_t)lc * NE1 * nu + u;
+    double* m2 = A.bsub + (size_t)lc * NB * nu + u;
+    const int L = A.nlyr, np = A.nprop, nmo = A.nmom;
+    const double* q = A.prop + ((size_t)s * L + (L - 1 - lc)) * np;
+    double ssa = np > 1 ? q[1] : 0.0;
+    if (ssa == 1.0) ssa = 1.0 - kDither;
+    const double f = nmo >= N ? q[1 + N] : 0.0;
+    const double om = ssa * (1.0 - f) / (1.0 - ssa * f);
+    const double rf = om / (1.0 - f);
+    const bool beam = fb > 0.0 && mu0 > 0.0;
+    double y0[N];
+    ylm_row<N>(m, beam ? mu0 : 0.0, y0);
+    const double fac = (m == 0 ? 1.0 : 2.0) * fb / (4.0 * kPi);
+    const double eb = beam ? fac * exp(-A.tauc[(size_t)lc * A.ns + sl] * rmu0) : 0.0;
+    const int par = m & 1;
+    const double* lam = &tab_r<NN>().lam[m][0][0];
+    double zs[NN], zd[NN], hh[NN];
+HD_RUNROLL
+    for (int i = 0; i < NN; ++i) {
+      const double zp = rr[(oZp + i) * HD_RS], zm = rr[(oZm + i) * HD_RS];
+      zs[i] = beam ? Qc.w[i] * (zp + zm) : 0.0;
+      zd[i] = beam ? Qc.w[i] * (zp - zm) : 0.0;
+      hh[i] = Qc.w[i] * rr[(oH + i) * HD_RS];
+    }
+#pragma nounroll
+    for (int l2 = 0; l2 < NN; ++l2) {
+HD_RUNROLL
+      for (int half = 0; half < 2; ++half) {  // 0: even part, 1: odd part
+        const int l = 2 * l2 + (half ? 1 - par : par);
+        const double chi = l == 0 ? 1.0 : (l <= nmo ? q[1 + l] : 0.0);
+        const double gl = (2 * l + 1) * (chi - f) * rf;
+        const double gh = 0.5 * gl;
+        const double yl0 = ((l + m) & 1) ? -y0[l] : y0[l];  // Y_l^m(-mu0)
+        double x[NN], sb = 0.0, st = 0.0;
+HD_RUNROLL
+        for (int i = 0; i < NN; ++i) {
+          const double lm = lam[l * NN + i];
+          x[i] = Qc.sd[i] * (gh * lm);
+          sb = fma(half ? zd[i] : zs[i], lm, sb);
+          st = half ? fma(hh[i], lm, st) : fma(Qc.w[i], lm, st);
+        }
+        double y[NN];
+        if (half == 0) {  // L^T x
+HD_RUNROLL
+          for (int k = 0; k < NN; ++k) {
+            double a = 0.0;
+HD_RUNROLL
+            for (int i = k; i < NN; ++i) a = fma(lch[i][k], x[i], a);
+            y[k] = a;
+          }
+        } else {  // L^-1 x
+HD_RUNROLL
+          for (int i = 0; i < NN; ++i) {
+            double t = x[i];
+HD_RUNROLL
+            for (int k = 0; k < i; ++k) t = fma(-lch[i][k], y[k], t);
+            y[i] = t * rd[i];
+          }
+        }
+        double* mo = half ? m2 : m1;
+HD_RUNROLL
+        for (int j = 0; j < NN; ++j) {
+          double a = 0.0;
+HD_RUNROLL
+          for (int i = 0; i < NN; ++i) a = fma(v[i][j], y[i], a);
+          mo[(size_t)(j * NN + l2) * nu] = a;
+        }
+        const double abv = fma(eb * gl, yl0, gh * sb);
+        m1[(size_t)(NN * NN + half * NN + l2) * nu] = abv;
+        if (half == 0) m1[(size_t)(NN * NN + 2 * NN + l2) * nu] = gh * st;
+        else m2[(size_t)(NN * NN + l2) * nu] = gh * st;
+      }
+    }
+  }
+#endif
 }
 
 // ============================================================================
@@ -1277,6 +1370,188 @@ HD_RUNROLL
   if (!isfinite(chk)) flag(A, s, kStNonFinite);
 }
 
+#ifndef HD_RAD_WIDE
+// ============================================================================
+// per-(unit, user angle) source-function integration from the const kernel's maps
+// (nstr <= 16): the layer's source projections are two NN x NN products with the
+// angle's Y_l^m row (ce = Me ye, cx = Mo yo) instead of hd_rad_user_kernel's
+// per-angle Legendre sums, triangular solve and V^T products; the beam and thermal
+// amplitudes are dot products.  Everything after that -- the whole-layer terms,
+// interior user depths, the scan over layers -- is hd_rad_user_kernel's.
+// ============================================================================
+#ifndef HD_RAD_UMAP_WAVES
+#define HD_RAD_UMAP_WAVES 2
+#endif
+template <int NN>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HD_RAD_UMAP_WAVES)))
+void hd_rad_user_map_kernel(RadArgs A) {
+  constexpr int N = 2 * NN;
+  constexpr int nsym = NN * (NN + 1) / 2;
+  constexpr int oZp = nsym + NN * NN + NN, oZm = oZp + NN, oH = oZm + NN, oBt = oH + NN;
+  constexpr int oEk = oBt + 4, oE0 = oEk + NN;
+  constexpr int NE1 = rad_layer_record_doubles(NN);
+  constexpr int NB = rad_bsub_doubles(NN);
+  const Quad<NN>& Qc = quad_r<NN>();
+  const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (long)A.ns * A.numu) return;
+  const int sl = (int)(id / A.numu);
+  const int iu = (int)(id - (long)sl * A.numu);
+  const int m = blockIdx.y;
+  const int u = m * A.ns + sl;
+  const long s = A.s0 + sl;
+  const int L = A.nlyr;
+  const size_t nu = A.nu;
+  const double muu = A.umu[iu];
+  const double mu0 = A.umu0 ? A.umu0[s] : 1.0;
+  const double fb = A.fbeam ? A.fbeam[s] : 0.0;
+  const bool beam = fb > 0.0 && mu0 > 0.0;
+  const double rmu0 = beam ? 1.0 / mu0 : 0.0;
+  const bool therm = A.planck && m == 0;
+  const int par = m & 1;
+  double ye[NN], yo[NN];
+  {
+    double yu[N];
+    ylm_row<N>(m, muu, yu);
+HD_RUNROLL
+    for (int l2 = 0; l2 < NN; ++l2) {
+      ye[l2] = yu[2 * l2 + par];
+      yo[l2] = yu[2 * l2 + 1 - par];
+    }
+  }
+  const bool up = muu > 0.0;
+
+  double cur = 0.0;
+  if (up) {
+    if (m == 0) {
+      const double* lv = A.lev + (size_t)L * 2 * NN * nu + u;
+      double fdn = 0.0;
+HD_RUNROLL
+      for (int i = 0; i < NN; ++i) fdn = fma(Qc.g[i] * Qc.g[i], lv[(NN + i) * nu], fdn);
+      fdn *= 2.0 * kPi;
+      const double alb = A.albedo ? A.albedo[s] : 0.0;
+      if (beam) {
+        const double tb = A.tauc[(size_t)(L - 1) * A.ns + sl] +
+                          HD_RREC(L - 1, u)[(oBt + 2) * HD_RS];
+        fdn += fb * mu0 * exp(-tb * rmu0);
+      }
+      cur = alb / kPi * fdn + (A.planck ? (1.0 - alb) * A.planckv[(size_t)(L + 1) * A.ns + sl]
+                                        : 0.0);
+    }
+  } else if (m == 0) {
+    cur = A.fisot ? A.fisot[s] : 0.0;
+    if (A.planck) cur += A.planckv[(size_t)(L + 2) * A.ns + sl];
+  }
+  int k = up ? A.ntau - 1 : 0;
+  double chk = 0.0;
+  for (int step = 0; step < L; ++step) {
+    const int lc = up ? L - 1 - step : step;
+    const double ttop = A.taus[(size_t)lc * A.ns + sl];
+    const double tbot = A.taus[(size_t)(lc + 1) * A.ns + sl];
+    const double* rr = HD_RREC(lc, u);
+    const double* m1 = A.rsw + (size_t)lc * NE1 * nu + u;
+    const double* m2 = A.bsub + (size_t)lc * NB * nu + u;
+    const double* co = A.cst + (size_t)lc * 2 * NN * nu + u;
+    const double bt = rr[oBt * HD_RS], slope = rr[(oBt + 1) * HD_RS], taup = rr[(oBt + 2) * HD_RS];
+    double kk[NN], hpl[NN], hmi[NN];
+HD_RUNROLL
+    for (int j = 0; j < NN; ++j) {
+      double ce = 0.0, cx = 0.0;
+HD_RUNROLL
+      for (int l2 = 0; l2 < NN; ++l2) {
+        ce = fma(m1[(size_t)(j * NN + l2) * nu], ye[l2], ce);
+        cx = fma(m2[(size_t)(j * NN + l2) * nu], yo[l2], cx);
+      }
+      kk[j] = rr[(nsym + NN * NN + j) * HD_RS];
+      cx *= -kk[j];
+      hpl[j] = co[j * nu] * (ce + cx);
+      hmi[j] = co[(NN + j) * nu] * (ce - cx);
+      // one row of the maps in flight at a time, consumed before the next row's loads
+      // (at two waves per SIMD the other wave covers the latency; with the products
+      // sunk below all 128 loads the kernel needed 490 registers)
+      asm volatile("" : "+v"(hpl[j]), "+v"(hmi[j])::"memory");
+    }
+    double ab = 0.0, a0 = 0.0, a1t = 0.0;
+    if (beam) {
+HD_RUNROLL
+      for (int l2 = 0; l2 < NN; ++l2) {
+        ab = fma(m1[(size_t)(NN * NN + l2) * nu], ye[l2], ab);
+        ab = fma(m1[(size_t)(NN * NN + NN + l2) * nu], yo[l2], ab);
+      }
+    }
+    if (therm) {
+      double we = 0.0, wo = 0.0;
+HD_RUNROLL
+      for (int l2 = 0; l2 < NN; ++l2) {
+        we = fma(m1[(size_t)(NN * NN + 2 * NN + l2) * nu], ye[l2], we);
+        wo = fma(m2[(size_t)(NN * NN + l2) * nu], yo[l2], wo);
+      }
+      const double om = rr[(oBt + 3) * HD_RS];
+      const double ce0 = (1.0 - om) + 2.0 * we;
+      a1t = slope * ce0;
+      a0 = fma(bt, ce0, 2.0 * slope * wo);
+    }
+    // general segment [t1 (evaluation), t2 (far end)] for user depths inside the layer
+    auto integ = [&](double t1, double t2) {
+      double r = 0.0;
+HD_RUNROLL
+      for (int j = 0; j < NN; ++j) {
+        r += seg_exp(hpl[j], kk[j], t1, t2, 0.0, muu);
+        r += seg_exp(hmi[j], -kk[j], t1, t2, taup, muu);
+        asm volatile("" : "+v"(r));  // one eigen-term at a time
+      }
+      if (beam) r += seg_exp(ab, rmu0, t1, t2, 0.0, muu);
+      if (therm) {
+        const double e2 = exp(-(t2 - t1) / muu);
+        r += (a0 + a1t * t1 + a1t * muu) - (a0 + a1t * t2 + a1t * muu) * e2;
+      }
+      return r;
+    };
+    const double anu = fabs(muu);
+    const double lmu = taup / anu;
+    const double emu = exp(-lmu);
+    double lay = 0.0;
+HD_RUNROLL
+    for (int j = 0; j < NN; ++j) {
+      const double ek = rr[(oEk + j) * HD_RS];
+      const double reg = (1.0 - ek * emu) / fma(kk[j], anu, 1.0);
+      const double sng = dexp(ek, emu, fma(-kk[j], anu, 1.0), lmu);
+      lay = up ? fma(hpl[j], reg, fma(hmi[j], sng, lay)) : fma(hpl[j], sng, fma(hmi[j], reg, lay));
+      asm volatile("" : "+v"(lay));  // one eigen-term's quotient and series at a time
+    }
+    if (beam) {
+      const double e0l = rr[oE0 * HD_RS];
+      lay += up ? ab * (1.0 - e0l * emu) / fma(anu, rmu0, 1.0)
+                : ab * dexp(e0l, emu, fma(-anu, rmu0, 1.0), lmu);
+    }
+    if (therm) {
+      lay += up ? (a0 + a1t * muu) - (a0 + a1t * taup + a1t * muu) * emu
+                : (a0 + a1t * taup + a1t * muu) - (a0 + a1t * muu) * emu;
+    }
+    const double cin = cur;
+    const double cout = fma(cin, emu, lay);
+    const double tau = tbot - ttop;
+    const double scale = tau > 0.0 ? taup / tau : 0.0;
+    auto at = [&](double t) {
+      const double tin = up ? taup : 0.0;
+      if (t == tin) return cin;
+      if (t == taup - tin) return cout;
+      return cin * exp(-fabs(tin - t) / anu) + integ(t, tin);
+    };
+    // the user depths in this layer, in ray order (one copy of the interior integral)
+    while (up ? (k >= 0 && user_tau(A, k, sl) >= ttop) : (k < A.ntau && user_tau(A, k, sl) <= tbot)) {
+      const double t = fmin(fmax((user_tau(A, k, sl) - ttop) * scale, 0.0), taup);
+      const double val = at(t);
+      A.radm[((size_t)k * A.numu + iu) * nu + u] = val;
+      chk += val;
+      k += up ? -1 : 1;
+    }
+    cur = cout;
+  }
+  for (; k < A.ntau && !up; ++k) A.radm[((size_t)k * A.numu + iu) * nu + u] = cur;
+  if (!isfinite(chk)) flag(A, s, kStNonFinite);
+}
+#endif
+
 // ============================================================================
 // uu[s][j][lu][iu] = sum_m I_m cos(m (phi_j - phi0))
 // ============================================================================
@@ -1550,6 +1825,15 @@ static bool rad_user_rolled() {
   return v;
 }
 
+// HD_RAD_USER=direct: nstr <= 16 user angles by the per-angle hd_rad_user_kernel
+static bool rad_user_direct() {
+  static const bool v = [] {
+    const char* e = ab_env("HD_RAD_USER");
+    return e && std::strcmp(e, "direct") == 0;
+  }();
+  return v;
+}
+
 template <int NN>
 static void launch_rad(const RadArgs& a, bool radiances, hipStream_t st) {
   const unsigned ns_b = (unsigned)((a.ns + 255) / 256);
@@ -1570,18 +1854,30 @@ static void launch_rad(const RadArgs& a, bool radiances, hipStream_t st) {
   // homogeneous constants (hd_team_mfma.hip), so the const kernel does not run
   const bool team_user =
       NN > kMaxRegNN && rad && a.numu <= rad_layer_record_doubles(NN) && !rad_user_rolled();
+  // nstr <= 16 with radiances: the const kernel writes the angle-independent maps and
+  // the user angles run hd_rad_user_map_kernel (HD_AB=1 HD_RAD_USER=direct: the
+  // per-angle hd_rad_user_kernel)
+  const bool umap = NN <= kMaxRegNN && rad && !rad_user_direct();
+  RadArgs ac = a;
+  ac.umap = umap ? 1 : 0;
   if (team_user) {
     (void)hd::launch_rad_team_user(NN, a, st);
   } else {
-    const long nc = (long)a.nu * a.nlyr;
-    hipLaunchKernelGGL(hd_rad_const_kernel<NN>, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0,
-                       st, a);
+    const long nc = (long)a.ns * a.nlyr;
+    hipLaunchKernelGGL(hd_rad_const_kernel<NN>, dim3((unsigned)((nc + 255) / 256), (unsigned)a.nm),
+                       dim3(256), 0, st, ac);
   }
   const long nf = (long)a.ns * a.ntau;
   hipLaunchKernelGGL(hd_rad_flux_kernel<NN>, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, st,
                      a);
   if (rad) {
     const long nr = (long)a.ns * a.numu;
+#ifndef HD_RAD_WIDE
+    if (umap)
+      hipLaunchKernelGGL(hd_rad_user_map_kernel<NN>, dim3((unsigned)((nr + 63) / 64), (unsigned)a.nm),
+                         dim3(64), 0, st, ac);
+    else
+#endif
     if (!team_user)
       hipLaunchKernelGGL(hd_rad_user_kernel<NN>, dim3((unsigned)((nr + 63) / 64), (unsigned)a.nm),
                          dim3(64), 0, st, a);

@@ -70,6 +70,10 @@ struct RadArgs {
   int max_sweeps;
   int numu, nphi, ntau;
   int corint;  // Nakajima-Tanaka TMS correction of the single scattering
+  // nstr <= 16 with radiances: the const kernel also writes each (unit, layer)'s
+  // angle-independent maps into the rsw / bsub regions (dead after the sweep) and the
+  // user-angle integration runs hd_rad_user_map_kernel
+  int umap;
   double* sink;  // team kernels: target of the stores a lane does not own (>= 64 doubles)
 };
 
