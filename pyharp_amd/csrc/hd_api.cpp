@@ -218,17 +218,19 @@ int ensure_rad_tables(hd_context* ctx) {
 
 long auto_chunk(long nsolve, int nn, int nlyr, bool planck) {
   // NN <= 8: the sweep runs one lane per solve at one wave per SIMD (its register
-  // file is full) and cannot share a SIMD with the layer kernel.  A chunk of about
-  // 40 000 solves (625 sweep waves) leaves ~40 % of the SIMDs to the next chunk's layer
-  // kernel while the sweep runs, instead of the 1 024 waves of a 65 536-solve chunk
-  // that take every SIMD: C4 12.80 -> 13.27 M solves/s (16 chunks of 40 000; 20 of
-  // 32 000: 13.35; 24-28 chunks: 12.96-13.03), the 8-GPU rank shape unchanged (2 x
-  // 40 000; 3 x 26 667 is slower), profiles/r05/chunk_sweep.txt.
+  // file is full) and cannot share a SIMD with the layer kernel.  Chunks of 32 000-
+  // 40 000 solves (500-625 sweep waves) leave 40-50 % of the SIMDs to the next chunk's
+  // layer kernel while a sweep runs, instead of the 1 024 waves of a 65 536-solve chunk
+  // that take every SIMD: C4 12.80 -> 13.35 M solves/s at 20 chunks of 32 000 (16 of
+  // 40 000: 13.27; 24-28 chunks: 12.96-13.03).  With fewer than five chunks the
+  // pipeline's fill and drain dominate and the larger chunk wins: the 8-GPU rank shape
+  // (80 000) runs 2 x 40 000 at 12.15 M, 3 x 26 667 at 11.78
+  // (profiles/r05/chunk_sweep.txt).
   // NN > 8: one 16-lane team per solve; chunks bounded by a scratch budget
   // (the rest of the 288 GB stays the caller's).
   long target;
   if (nn <= hd::kMaxRegNN) {
-    target = 40960;
+    target = (nsolve + 32767) / 32768 >= 5 ? 32768 : 40960;
   } else {
     // bytes of scratch for the two chunks in flight (the per-solve size counts both)
     const double budget = 16.0 * 1024.0 * 1024.0 * 1024.0;

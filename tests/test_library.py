@@ -290,14 +290,16 @@ def test_night_side_beam():
 
 def test_chunk_plan(lib):
     """The automatic chunking (hd_chunk_solves; no device needed).  Register path
-    (nstr <= 16): ~40 960 solves per chunk, so that the next chunk's layer kernel keeps
-    ~40 % of the SIMDs while a chunk's sweep runs -- C4 640 000 solves in 16 chunks
-    (profiles/r05/chunk_sweep.txt), the 8-GPU rank shape 80 000 in 2.  Team path (nstr 18..32): a 16 GB
+    (nstr <= 16): chunks of ~32 768 solves (~40 960 when that gives fewer than five), so
+    that the next chunk's layer kernel keeps 40-50 % of the SIMDs while a chunk's sweep
+    runs -- C4 640 000 solves in 20 chunks, the 8-GPU rank shape 80 000 in 2
+    (profiles/r05/chunk_sweep.txt).  Team path (nstr 18..32): a 16 GB
     scratch budget bounds the chunk (C5 64 000 solves: 4 chunks of 16 000); the 8-GPU
     C5 rank shape (8 g-points x 1 000 columns) stays one chunk -- split in two it ran
     9 % slower (profiles/r05/c5_rank_shape.txt)."""
     from pyharp_amd import _lib
-    assert _lib.chunk_solves(16, 80, 640000) == 40000
+    assert _lib.chunk_solves(16, 80, 640000) == 32000
+    assert _lib.chunk_solves(16, 80, 160000) == 32000
     assert _lib.chunk_solves(16, 80, 65536) == 32768
     assert _lib.chunk_solves(16, 80, 80000) == 40000
     assert _lib.chunk_solves(16, 80, 16) == 16
