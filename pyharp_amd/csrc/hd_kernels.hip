@@ -896,12 +896,14 @@ __device__ __forceinline__ void backsub_body(const SweepArgs& A);
 // K1+K2+K3 in one pass per solve (the column kernel): one lane walks its solve's
 // layers top -> bottom, runs each layer's setup (layer_body) into registers and
 // feeds it straight to the adding sweep (sweep_body), then walks back up through
-// the back-substitution records it wrote (backsub_body).  Bitwise the same
-// arithmetic as hd_layer_kernel + hd_sweep_kernel + the back-substitution, but the
+// the back-substitution records it wrote (backsub_body).  The same source
+// arithmetic as hd_layer_kernel + hd_sweep_kernel + the back-substitution (to
+// rounding: the compiler may contract differently in the fused body), but the
 // layer records (RecL: 90 doubles per (solve, layer), written once and read once)
 // never reach HBM, and the three kernels' time-sharing of the SIMDs -- neither
 // the layer kernel nor the sweep leaves room on a SIMD for the other -- becomes
-// one instruction stream per wave.
+// one instruction stream per wave.  Measured slower at one wave per SIMD (A/B
+// only, HD_COLUMN; profiles/r05/column_ab.txt).
 // ============================================================================
 template <int NN>
 __global__ __launch_bounds__(64) void hd_column_kernel(LayerArgs LA, SweepArgs A) {
