@@ -162,7 +162,7 @@ struct ColRec {
 };
 
 // The layer setup of (solve s, solver layer lc) into the record sink `out`
-// (PairOut: RecL in HBM; RegRec: registers).  psi_lds: this wave's Psi^T
+// (PairOut: RecL in HBM; ColRec: on chip).  psi_lds: this wave's Psi^T
 // staging, element e of lane lt at e * kLayerBlock + lt.  Returns the status bits.
 // OPQ: the quadrature table through quad_opaque (the column kernel's layer loop)
 template <int NN, bool OPQ, class Out>
@@ -563,7 +563,7 @@ __device__ __forceinline__ int layer_body(const LayerArgs& A, long s, int sl, in
   return st;
 }
 
-template <int NN>
+template <int NN, bool NT>
 __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
   __shared__ double psi_lds[psi_doubles<NN>() * kLayerBlock];  // Psi^T staged per lane
   // block = 64 consecutive solves (one wave each) x kLayersPerBlock consecutive
@@ -586,8 +586,8 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
   const int lc = tl * kLayersPerBlock + (lt >> 6);  // solver layer, 0 = top
   if (sl >= A.nsc || lc >= A.nlyr) return;
   const long s = solve_of(A.s0 + sl, A.cmaj, A.nwave, A.ncol);
-  PairOut out{reinterpret_cast<double2*>(A.scr) + (size_t)lc * RecL<NN>::pairs * A.nsc + sl,
-              (size_t)A.nsc, 0.0};
+  PairOutT<NT> out{reinterpret_cast<double2*>(A.scr) + (size_t)lc * RecL<NN>::pairs * A.nsc + sl,
+                   (size_t)A.nsc, 0.0};
   const int st = layer_body<NN, false>(A, s, sl, lc, psi_lds, lt, out);
   if (st) {
     atomicOr(&A.status[s], st);
@@ -603,7 +603,7 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
 // loads from the HBM record; hd_column_kernel: the layer setup run right there
 // into registers).  Stores the back-substitution records, the surface level and
 // x; returns the status bits.
-template <int NN, class RecAt>
+template <int NN, bool NT, class RecAt>
 __device__ __forceinline__ int sweep_body(const SweepArgs& A, long sl, long s, RecAt&& rec_at) {
   const Quad<NN>& Qc = quad<NN>();
   const int L = A.nlyr;
@@ -640,7 +640,7 @@ __device__ __forceinline__ int sweep_body(const SweepArgs& A, long sl, long s, R
     using RL = RecL<NN>;
     using RB = RecB<NN>;
     auto rec = rec_at(lc);
-    PairOut bp{reinterpret_cast<double2*>(A.bsub) + (size_t)lc * RB::pairs * nsc + sl, nsc, 0.0};
+    PairOutT<NT> bp{reinterpret_cast<double2*>(A.bsub) + (size_t)lc * RB::pairs * nsc + sl, nsc, 0.0};
     // this layer's R~ (upper) and S~+ ; each record element is read once
     double rl[NN][NN], spl[NN];
     {
@@ -871,7 +871,7 @@ __device__ __forceinline__ int sweep_body(const SweepArgs& A, long sl, long s, R
   return st;
 }
 
-template <int NN>
+template <int NN, bool NT>
 __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
   const long sl = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (sl >= A.nsc) return;
@@ -880,16 +880,16 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
   auto rec_at = [&](int lc) {
     const double2* lp =
         reinterpret_cast<const double2*>(A.scr) + (size_t)lc * RecL<NN>::pairs * nsc + sl;
-    return [lp, nsc](int e) { return pair_get(lp, nsc, e); };
+    return [lp, nsc](int e) { return pair_get<NT>(lp, nsc, e); };
   };
-  const int st = sweep_body<NN>(A, sl, s, rec_at);
+  const int st = sweep_body<NN, NT>(A, sl, s, rec_at);
   if (st) {
     atomicOr(&A.status[s], st);
     if (st & 0x0F) atomicOr(A.anyerr, 1);
   }
 }
 
-template <int NN, bool PRE>
+template <int NN, bool PRE, bool NT>
 __device__ __forceinline__ void backsub_body(const SweepArgs& A);
 
 // ============================================================================
@@ -920,7 +920,7 @@ __global__ __launch_bounds__(64) void hd_column_kernel(LayerArgs LA, SweepArgs A
       lst |= layer_body<NN, true>(LA, s, (int)sl, lc, psi_lds, lt, r);
       return [&r](int e) { return r.get(e); };
     };
-    const int st = sweep_body<NN>(A, sl, s, rec_at) | lst;
+    const int st = sweep_body<NN, false>(A, sl, s, rec_at) | lst;
     if (st) {
       atomicOr(&A.status[s], st);
       if (st & 0x0F) atomicOr(A.anyerr, 1);
@@ -929,7 +929,7 @@ __global__ __launch_bounds__(64) void hd_column_kernel(LayerArgs LA, SweepArgs A
   // the back-substitution reads what this wave wrote (with the band epilogue, lanes
   // past the chunk read the last solve's records)
   __syncthreads();
-  backsub_body<NN, true>(A);
+  backsub_body<NN, true, false>(A);
 }
 
 // ============================================================================
@@ -1507,7 +1507,7 @@ __global__ __launch_bounds__(64) void hd_sweep_quad_kernel(SweepArgs A) {
 // The arithmetic of both back-substitution kernels (identical expression order,
 // so a solve's fluxes do not depend on which kernel ran its chunk).  PRE: the
 // next layer's record is loaded into registers before this layer is computed.
-template <int NN, bool PRE>
+template <int NN, bool PRE, bool NT>
 __device__ __forceinline__ void backsub_body(const SweepArgs& A) {
   const Quad<NN>& Qc = quad<NN>();
   const long lane_sl = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1606,13 +1606,13 @@ __device__ __forceinline__ void backsub_body(const SweepArgs& A) {
     {
       const double2* bp = rec_ptr(L - 1);
 #pragma unroll
-      for (int e = 0; e < NP; ++e) cur[e] = bp[e * nsc];
+      for (int e = 0; e < NP; ++e) cur[e] = rec_load<NT>(bp + e * nsc);
     }
     for (int lc = L - 1; lc >= 0; --lc) {
       if (lc > 0) {
         const double2* bp = rec_ptr(lc - 1);
 #pragma unroll
-        for (int e = 0; e < NP; ++e) nxt[e] = bp[e * nsc];
+        for (int e = 0; e < NP; ++e) nxt[e] = rec_load<NT>(bp + e * nsc);
       }
       layer(lc, [&](int e) { return (e & 1) ? cur[e >> 1].y : cur[e >> 1].x; });
 #pragma unroll
@@ -1621,7 +1621,7 @@ __device__ __forceinline__ void backsub_body(const SweepArgs& A) {
   } else {
     for (int lc = L - 1; lc >= 0; --lc) {
       const double2* bp = rec_ptr(lc);
-      layer(lc, [&](int e) { return pair_get(bp, nsc, e); });
+      layer(lc, [&](int e) { return pair_get<NT>(bp, nsc, e); });
     }
   }
   if (live && !isfinite(chk)) {
@@ -1639,19 +1639,19 @@ __device__ __forceinline__ void backsub_body(const SweepArgs& A) {
 // layer-kernel wave as long as that one stays at <= 416 (410 now).  The 16-byte
 // record loads want the registers of a whole pair set in flight (8 waves per SIMD,
 // 64 VGPRs, spilled).
-template <int NN>
+template <int NN, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5)))
 void hd_backsub_kernel(SweepArgs A) {
-  backsub_body<NN, false>(A);
+  backsub_body<NN, false, NT>(A);
 }
 
 // K3 for the last chunk of a call, which nothing overlaps: no occupancy cap,
 // a whole layer record in flight at once and the next one loaded while this
 // one is computed (the capped kernel issues the 81 loads of a layer in small
 // register-limited batches, each waiting out a memory latency).
-template <int NN>
+template <int NN, bool NT>
 __global__ __launch_bounds__(64) void hd_backsub_tail_kernel(SweepArgs A) {
-  backsub_body<NN, true>(A);
+  backsub_body<NN, true, NT>(A);
 }
 
 // ============================================================================
@@ -1862,8 +1862,12 @@ static void launch_sweep(const SweepArgs& sa, hipStream_t stream) {
       return;
     }
   }
-  hipLaunchKernelGGL(hd_sweep_kernel<NN>, dim3((unsigned)((sa.nsc + 63) / 64)), dim3(64), 0,
-                     stream, sa);
+  if (sa.nsc >= kNtMinSolves)
+    hipLaunchKernelGGL((hd_sweep_kernel<NN, true>), dim3((unsigned)((sa.nsc + 63) / 64)), dim3(64),
+                       0, stream, sa);
+  else
+    hipLaunchKernelGGL((hd_sweep_kernel<NN, false>), dim3((unsigned)((sa.nsc + 63) / 64)), dim3(64),
+                       0, stream, sa);
 }
 
 template <int NN>
@@ -1873,7 +1877,10 @@ static hipError_t launch_chunk(const PlanckArgs* pa, const TaucArgs* ta, const L
   const unsigned nb1 = (unsigned)(((la.nsc + 63) / 64) *
                                   ((la.nlyr + kLayersPerBlock - 1) / kLayersPerBlock));
   if (ev) (void)hipEventRecord(ev[0], stream);
-  hipLaunchKernelGGL(hd_layer_kernel<NN>, dim3(nb1), dim3(kLayerBlock), 0, stream, la);
+  if (la.nsc >= kNtMinSolves)
+    hipLaunchKernelGGL((hd_layer_kernel<NN, true>), dim3(nb1), dim3(kLayerBlock), 0, stream, la);
+  else
+    hipLaunchKernelGGL((hd_layer_kernel<NN, false>), dim3(nb1), dim3(kLayerBlock), 0, stream, la);
   if (ev) (void)hipEventRecord(ev[1], stream);
   launch_sweep<NN>(sa, stream);
   if (ev) (void)hipEventRecord(ev[2], stream);
@@ -1882,12 +1889,12 @@ static hipError_t launch_chunk(const PlanckArgs* pa, const TaucArgs* ta, const L
 
 template <int NN>
 static void launch_backsub(const SweepArgs& sa, hipStream_t stream, bool tail) {
-  if (tail)
-    hipLaunchKernelGGL(hd_backsub_tail_kernel<NN>, dim3((unsigned)((sa.nsc + 63) / 64)), dim3(64),
-                       0, stream, sa);
-  else
-    hipLaunchKernelGGL(hd_backsub_kernel<NN>, dim3((unsigned)((sa.nsc + 255) / 256)), dim3(256),
-                       0, stream, sa);
+  const dim3 gt((unsigned)((sa.nsc + 63) / 64)), gc((unsigned)((sa.nsc + 255) / 256));
+  const bool nt = sa.nsc >= kNtMinSolves;
+  if (tail && nt) hipLaunchKernelGGL((hd_backsub_tail_kernel<NN, true>), gt, dim3(64), 0, stream, sa);
+  else if (tail) hipLaunchKernelGGL((hd_backsub_tail_kernel<NN, false>), gt, dim3(64), 0, stream, sa);
+  else if (nt) hipLaunchKernelGGL((hd_backsub_kernel<NN, true>), gc, dim3(256), 0, stream, sa);
+  else hipLaunchKernelGGL((hd_backsub_kernel<NN, false>), gc, dim3(256), 0, stream, sa);
 }
 
 hipError_t launch_backsub_nn(int nn, const SweepArgs& sa, hipStream_t stream, bool tail) {
@@ -1925,7 +1932,10 @@ template <int NN>
 static void launch_layer(const LayerArgs& la, hipStream_t stream) {
   const unsigned nb1 = (unsigned)(((la.nsc + 63) / 64) *
                                   ((la.nlyr + kLayersPerBlock - 1) / kLayersPerBlock));
-  hipLaunchKernelGGL(hd_layer_kernel<NN>, dim3(nb1), dim3(kLayerBlock), 0, stream, la);
+  if (la.nsc >= kNtMinSolves)
+    hipLaunchKernelGGL((hd_layer_kernel<NN, true>), dim3(nb1), dim3(kLayerBlock), 0, stream, la);
+  else
+    hipLaunchKernelGGL((hd_layer_kernel<NN, false>), dim3(nb1), dim3(kLayerBlock), 0, stream, la);
 }
 
 hipError_t launch_layer_nn(int nn, const LayerArgs& la, hipStream_t stream) {

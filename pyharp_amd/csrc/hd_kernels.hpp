@@ -44,22 +44,66 @@ struct RecB {  // back-substitution record: ZT (column-major) | t | rc | cs
   static constexpr int Cs = Rc + even_up(NN);
   static constexpr int pairs = (Cs + 2) / 2;
 };
+// Record traffic (layer records, back-substitution records) of a large chunk is written
+// once and read once, a whole kernel later, far beyond what the caches hold: there the
+// kernels use nontemporal loads and stores (the `nt` bit, NT = true) so that it does not
+// displace anything else -- C4 +2 %, the 8-GPU rank shape +1.6 % in interleaved runs.  A
+// small chunk's records stay in L2 between its kernels and plain accesses keep them there
+// (C1: 146 k vs 137 k solves/s with nt).  The team path (nstr 18..32) keeps plain
+// accesses: its records are read in 8-byte pieces by a team's lanes, and with nt C5 ran
+// 1.07 M solves/s against 1.33 M.  profiles/r05/record_nt_ab.txt
+#ifndef HD_NT_MIN_SOLVES
+#define HD_NT_MIN_SOLVES 16384
+#endif
+constexpr int kNtMinSolves = HD_NT_MIN_SOLVES;  // chunks of at least this many solves use NT
+typedef double hd_d2v __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ void rec_store(double2* p, double2 v) {
+  if constexpr (NT) {
+    hd_d2v w = {v.x, v.y};
+    __builtin_nontemporal_store(w, reinterpret_cast<hd_d2v*>(p));
+  } else {
+    *p = v;
+  }
+}
+template <bool NT>
+__device__ __forceinline__ double2 rec_load(const double2* p) {
+  if constexpr (NT) {
+    const hd_d2v w = __builtin_nontemporal_load(reinterpret_cast<const hd_d2v*>(p));
+    return make_double2(w.x, w.y);
+  } else {
+    return *p;
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void rec_st(double* p, double v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+template <bool NT>
+__device__ __forceinline__ double rec_ld(const double* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
 // writes record elements in increasing order within a group as 16-byte pairs
-struct PairOut {
+template <bool NT>
+struct PairOutT {
   double2* p;
   size_t stride;  // pairs -> double2 stride (nsc)
   double pend;
   __device__ __forceinline__ void put(int e, double v) {
-    if (e & 1) p[(size_t)(e >> 1) * stride] = make_double2(pend, v);
+    if (e & 1) rec_store<NT>(p + (size_t)(e >> 1) * stride, make_double2(pend, v));
     else pend = v;
   }
   // after the group's last element e: a lone even element goes out with a zero pad
   __device__ __forceinline__ void close(int e) {
-    if (!(e & 1)) p[(size_t)(e >> 1) * stride] = make_double2(pend, 0.0);
+    if (!(e & 1)) rec_store<NT>(p + (size_t)(e >> 1) * stride, make_double2(pend, 0.0));
   }
 };
+using PairOut = PairOutT<false>;
+template <bool NT = false>
 __device__ __forceinline__ double pair_get(const double2* p, size_t stride, int e) {
-  const double2 q = p[(size_t)(e >> 1) * stride];
+  const double2 q = rec_load<NT>(p + (size_t)(e >> 1) * stride);
   return (e & 1) ? q.y : q.x;
 }
 

@@ -18,6 +18,7 @@ import csv
 import glob
 import json
 import os
+import re
 
 
 def per_kernel(run_dir, counter):
@@ -32,6 +33,8 @@ def per_kernel(run_dir, counter):
             if not name.startswith(("void hd::", "hd::")):
                 continue
             key = name.split("(")[0].replace("void ", "").replace("hd::", "")
+            # the record-access variant (NT template argument) is one kernel here
+            key = re.sub(r",\s*(true|false)>", ">", key)
             acc.setdefault(key, []).append(float(r["Counter_Value"]) * 1024.0)
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
