@@ -49,11 +49,12 @@ struct RecB {  // back-substitution record: ZT (column-major) | t | rc | cs
 // kernels use nontemporal loads and stores (the `nt` bit, NT = true) so that it does not
 // displace anything else -- C4 +2 %, the 8-GPU rank shape +1.6 % in interleaved runs.  A
 // small chunk's records stay in L2 between its kernels and plain accesses keep them there
-// (C1: 146 k vs 137 k solves/s with nt).  The team path (nstr 18..32) keeps plain
-// accesses: its records are read in 8-byte pieces by a team's lanes, and with nt C5 ran
-// 1.07 M solves/s against 1.33 M.  profiles/r05/record_nt_ab.txt
+// (C1: 146 k vs 137 k solves/s with nt).  The team path (nstr 18..32) uses nt for its
+// whole-row record stores only (C5 +1.3 %): its record reads are 8-byte pieces of a
+// team's lanes, and with nt on them C5 ran 1.07 M solves/s against 1.33 M.
+// profiles/r05/record_nt_ab.txt
 #ifndef HD_NT_MIN_SOLVES
-#define HD_NT_MIN_SOLVES 16384
+#define HD_NT_MIN_SOLVES 4096  // records of >= ~230 MB per chunk: far beyond the 32 MB of L2
 #endif
 constexpr int kNtMinSolves = HD_NT_MIN_SOLVES;  // chunks of at least this many solves use NT
 typedef double hd_d2v __attribute__((ext_vector_type(2)));

@@ -213,7 +213,7 @@ __device__ __forceinline__ double team_matvec(const double (&xr)[NN], double x) 
 // ============================================================================
 // K1 (team, MFMA): per-(solve, layer) setup, four problems per wave
 // ============================================================================
-template <int NN>
+template <int NN, bool NT>
 __global__ __launch_bounds__(64, 2) void hd_team_mfma_layer_kernel(LayerArgs A) {
   __shared__ double lds[2 * kSet + 4 * 2 * 16];
   double* S0 = lds;
@@ -532,9 +532,11 @@ __global__ __launch_bounds__(64, 2) void hd_team_mfma_layer_kernel(LayerArgs A) 
       const int r = h + 4 * m;
       const double rr = Ap[tt][m] - Am[tt][m];
       const double tr = (Am[tt][m] + Ap[tt][m]) - (r == c ? 1.0 : 0.0);
+      // whole 128-B rows per problem: nontemporal for a large chunk (hd_kernels.hpp);
+      // the team reads stay plain (8-byte pieces: with nt C5 ran 20 % slower)
       if (ok && r < NN && c < NN) {
-        rec[r * NN + c] = rr;
-        rec[NN * NN + r * NN + c] = tr;
+        rec_st<NT>(&rec[r * NN + c], rr);
+        rec_st<NT>(&rec[NN * NN + r * NN + c], tr);
       }
       chk += rr + tr;
     }
@@ -852,7 +854,7 @@ __global__ __launch_bounds__(64, 1) void hd_team_mfma_sweep_kernel(SweepArgs A) 
 // The arithmetic and its order are hd_team_mfma_sweep_kernel's, so the records
 // and fluxes are bitwise the same (tests/test_gpu_parity.py: lean vs default).
 // ============================================================================
-template <int NN>
+template <int NN, bool NT>
 __global__ __launch_bounds__(64, 2) void hd_team_mfma_sweep_lean_kernel(SweepArgs A) {
   __shared__ double lds[2 * kSet];
   double* S0 = lds;
@@ -1074,7 +1076,7 @@ __global__ __launch_bounds__(64, 2) void hd_team_mfma_sweep_lean_kernel(SweepArg
         for (int m = 0; m < 4; ++m) {
           const int r = h + 4 * m;
           // branch-free: an element the lane does not own goes to the sink
-          *((ok && r < NN && c < NN) ? zr + r * NN + c : A.sink + lane) = zm[tt][m];
+          rec_st<NT>((ok && r < NN && c < NN) ? zr + r * NN + c : A.sink + lane, zm[tt][m]);
         }
       }
 #pragma unroll
@@ -1824,15 +1826,20 @@ hipError_t upload_quad_tables_team_mfma(const QuadTablesTeam& t) {
 template <int NN>
 static hipError_t launch_layer(const LayerArgs& la, hipStream_t stream) {
   const unsigned nb1 = (unsigned)(((la.nsc + 3) / 4) * (long)la.nlyr);
-  hipLaunchKernelGGL(hd_team_mfma_layer_kernel<NN>, dim3(nb1), dim3(64), 0, stream, la);
+  if (la.nsc >= kNtMinSolves)
+    hipLaunchKernelGGL((hd_team_mfma_layer_kernel<NN, true>), dim3(nb1), dim3(64), 0, stream, la);
+  else
+    hipLaunchKernelGGL((hd_team_mfma_layer_kernel<NN, false>), dim3(nb1), dim3(64), 0, stream, la);
   return hipGetLastError();
 }
 
 template <int NN>
 static hipError_t launch_sweep(const SweepArgs& sa, hipStream_t stream) {
-  if (sa.lean)
-    hipLaunchKernelGGL(hd_team_mfma_sweep_lean_kernel<NN>, dim3((unsigned)((sa.nsc + 3) / 4)),
-                       dim3(64), 0, stream, sa);
+  const dim3 gl((unsigned)((sa.nsc + 3) / 4));
+  if (sa.lean && sa.nsc >= kNtMinSolves)
+    hipLaunchKernelGGL((hd_team_mfma_sweep_lean_kernel<NN, true>), gl, dim3(64), 0, stream, sa);
+  else if (sa.lean)
+    hipLaunchKernelGGL((hd_team_mfma_sweep_lean_kernel<NN, false>), gl, dim3(64), 0, stream, sa);
   else
     hipLaunchKernelGGL(hd_team_mfma_sweep_kernel<NN>, dim3((unsigned)((sa.nsc + 3) / 4)), dim3(64),
                        0, stream, sa);
