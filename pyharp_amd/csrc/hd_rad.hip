@@ -38,6 +38,12 @@ namespace wide {
 namespace {
 
 constexpr int kLayerBlockR = 256;
+// the layer kernel's records (operators for the sweep, radiance records for the const,
+// flux and user kernels): whole-line stores, read a kernel later -- nontemporal
+#ifndef HD_RAD_NT
+#define HD_RAD_NT 1
+#endif
+constexpr bool kRadNt = HD_RAD_NT != 0;
 constexpr int kLayersPerBlockR = kLayerBlockR / 64;
 
 // nstr <= 16 (NN <= 8, this translation unit): every NN-loop fully unrolled,
@@ -372,28 +378,28 @@ HD_RUNROLL
     lower_t_solve<NN>(lch, rdl, cvec);
 HD_RUNROLL
     for (int i = 0; i < NN; ++i) {
-      rr[(oH + i) * nu] = Qc.rg[i] * cvec[i];
+      rec_st<kRadNt>(&rr[(oH + i) * nu], Qc.rg[i] * cvec[i]);
       cvec[i] = fma(b1 * Qc.rg[i], cvec[i], db);
     }
-    rr[oBt * nu] = bt;
-    rr[oSl * nu] = 0.5 * b1;
+    rec_st<kRadNt>(&rr[oBt * nu], bt);
+    rec_st<kRadNt>(&rr[oSl * nu], 0.5 * b1);
   } else {
 HD_RUNROLL
     for (int i = 0; i < NN; ++i) {
       cvec[i] = 0.0;
-      rr[(oH + i) * nu] = 0.0;
+      rec_st<kRadNt>(&rr[(oH + i) * nu], 0.0);
     }
-    rr[oBt * nu] = 0.0;
-    rr[oSl * nu] = 0.0;
+    rec_st<kRadNt>(&rr[oBt * nu], 0.0);
+    rec_st<kRadNt>(&rr[oSl * nu], 0.0);
   }
-  rr[oTp * nu] = taup;
-  rr[oOm * nu] = om;
+  rec_st<kRadNt>(&rr[oTp * nu], taup);
+  rec_st<kRadNt>(&rr[oOm * nu], om);
   {  // L (packed lower, row-major)
     int e = 0;
 HD_RUNROLL
     for (int i = 0; i < NN; ++i)
 HD_RUNROLL
-      for (int k = 0; k <= i; ++k) rr[(e++) * nu] = lch[i][k];
+      for (int k = 0; k <= i; ++k) rec_st<kRadNt>(&rr[(e++) * nu], lch[i][k]);
   }
 
   // ---- eigenpairs (hd_layer_kernel's form): C C^T = -A+, Sym = B^T B for
@@ -420,7 +426,7 @@ HD_RUNROLL
     for (int i = 0; i < NN; ++i) k2 = fma(v[i][j], v[i][j], k2);
     if (!(k2 > 0.0)) st |= kStEigen;
     kk[j] = sqrt(k2 > 0.0 ? k2 : 0.0);
-    rr[(oK + j) * nu] = kk[j];
+    rec_st<kRadNt>(&rr[(oK + j) * nu], kk[j]);
   }
 HD_RUNROLL
   for (int j = 0; j < NN; ++j) {  // U = C^-T B, column by column
@@ -477,8 +483,8 @@ HD_RUNROLL
   }
 HD_RUNROLL
   for (int i = 0; i < NN; ++i) {
-    rr[(oZp + i) * nu] = zp[i];
-    rr[(oZm + i) * nu] = zm[i];
+    rec_st<kRadNt>(&rr[(oZp + i) * nu], zp[i]);
+    rec_st<kRadNt>(&rr[(oZm + i) * nu], zm[i]);
   }
 
   // ---- layer operators in the flux-weighted basis (as hd_layer_kernel) ----
@@ -491,9 +497,9 @@ HD_RUNROLL
     const double delta = x > 1.0e-8 ? th * rcp_nr(kk[j] > 0.0 ? kk[j] : 1.0) : 0.5 * taup;
     dsq[j] = sqrt(delta);
     gsq[j] = sqrt(kk[j] * th);
-    rr[(oEk + j) * nu] = 1.0 - mm;  // exp(-k tau') for the user-angle kernel
+    rec_st<kRadNt>(&rr[(oEk + j) * nu], 1.0 - mm);  // exp(-k tau') for the user-angle kernel
   }
-  rr[oE0 * nu] = e0;
+  rec_st<kRadNt>(&rr[oE0 * nu], e0);
 HD_RUNROLL
   for (int j = 0; j < NN; ++j) {  // V = L^-1 U (stored), Psi^T = L^-T V Gamma^1/2 -> LDS
     double x[NN];
@@ -501,7 +507,7 @@ HD_RUNROLL
     for (int i = 0; i < NN; ++i) x[i] = v[i][j];
     lower_solve<NN>(lch, rdl, x);
 HD_RUNROLL
-    for (int i = 0; i < NN; ++i) rr[(oV + i * NN + j) * nu] = x[i];
+    for (int i = 0; i < NN; ++i) rec_st<kRadNt>(&rr[(oV + i * NN + j) * nu], x[i]);
     lower_t_solve<NN>(lch, rdl, x);
 HD_RUNROLL
     for (int i = 0; i < NN; ++i) psi_at(i * NN + j) = x[i] * gsq[j];
@@ -578,8 +584,8 @@ HD_RUNROLL
       for (int j = i; j < NN; ++j) {
         const double r = ap_[i][j] - am_[i][j];
         const double t = (am_[i][j] + ap_[i][j]) - ((i == j) ? 1.0 : 0.0);
-        out[e * nu] = r;
-        out[(nsym + e) * nu] = t;
+        rec_st<kRadNt>(&out[e * nu], r);
+        rec_st<kRadNt>(&out[(nsym + e) * nu], t);
         chk += r + t;
         ++e;
       }
@@ -588,11 +594,11 @@ HD_RUNROLL
   for (int i = 0; i < NN; ++i) {
     const double sp = Qc.g[i] * (zp[i] * (1.0 - e0) - db) + pvec[i] - qvec[i];
     const double sm = Qc.g[i] * (-zm[i] * (1.0 - e0) + db) - pvec[i] - qvec[i];
-    out[(2 * nsym + i) * nu] = sp;
-    out[(2 * nsym + NN + i) * nu] = sm;
+    rec_st<kRadNt>(&out[(2 * nsym + i) * nu], sp);
+    rec_st<kRadNt>(&out[(2 * nsym + NN + i) * nu], sm);
     chk += sp + sm;
   }
-  out[(2 * nsym + 2 * NN) * nu] = taup;
+  rec_st<kRadNt>(&out[(2 * nsym + 2 * NN) * nu], taup);
   if (!isfinite(chk + taup)) st |= kStNonFinite;
   flag(A, s, st);
 }

@@ -14,6 +14,7 @@
 #   sq=NAME[:NSTR]       SQ instruction-mix / MFMA / LDS passes over scripts/pmc_run.py
 #   rad=NAME[:ARGS]      python scripts/bench_rad.py ARGS  > rad_NAME.json
 #   radstats=NAME[:ARGS] rocprofv3 --kernel-trace --stats of scripts/bench_rad.py ARGS
+#   radsq=NAME[:ARGS]    SQ / FETCH_SIZE passes (one --pmc pass each) over one bench_rad.py step
 # ARGS are comma-separated (bench=c5:--config,c5,--steps,5).
 set -e -o pipefail
 TAG=${1:?tag}; shift
@@ -88,6 +89,15 @@ for step in "$@"; do
         --output-format csv -- python3 scripts/bench_rad.py $(args_of "$rest") \
         > "$OUT/radstats_$name.json" 2> "$OUT/radstats_$name.err" || { tail -20 "$OUT/radstats_$name.err"; exit 1; }
       cat "$OUT/radstats_$name.json" ;;
+    radsq)
+      for p in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" \
+               "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SALU SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_LDS SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64" \
+               "FETCH_SIZE"; do
+        d="$OUT/radsq_${name}_$(echo $p | cut -d' ' -f1)"
+        say "pmc $d: $p"
+        timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $p -d "$d" -o pmc --output-format csv \
+          -- python3 scripts/bench_rad.py --steps 1 --warmup 0 $(args_of "$rest") > "$d.log" 2>&1
+      done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
