@@ -347,17 +347,21 @@ import sys, numpy as np
 sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + '/tests')
 from test_gpu_radiance import _user_case
 np.save(sys.argv[5], _user_case(int(sys.argv[2]), sys.argv[3] == '1', sys.argv[4] == '1',
-                                int(sys.argv[6])))
+                                int(sys.argv[6]), int(sys.argv[7])))
 """
 
 
-def _user_case(nstr, planck, usrtau, nwave=2):
+def _user_case(nstr, planck, usrtau, nwave=2, nang=9):
     rng = np.random.default_rng(3100 + nstr + 10 * planck + 20 * usrtau)
     ncol, nlyr = 5, 9
     prop, bc, kw = _random_case(rng, nwave, ncol, nlyr, nstr, planck)
     total = prop[..., 0].sum(axis=-1).min()
     utau = np.sort(np.concatenate([[0.0, total], rng.uniform(0, total, 4)])) if usrtau else None
     umu = [-1.0, -0.7, -0.31, -0.12, 0.1, 0.37, 0.66, 0.93, 1.0]
+    if nang == 8:
+        umu.remove(0.66)
+    elif nang == 4:
+        umu = [-0.7, -0.12, 0.37, 1.0]
     d = _disort(nstr, nlyr, nwave, ncol, flags="lamber,quiet,usrang" + (",usrtau" if usrtau else ""),
                 umu=umu, phi=[0.0, 90.0], utau=utau, planck=planck, wl=kw.get("wave_lower"),
                 wu=kw.get("wave_upper"))
@@ -385,7 +389,7 @@ def test_team_user_kernel_matches_rolled(nstr, planck, usrtau, nwave, tmp_path):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, HD_AB="1", HD_RAD_USER="rolled")
     subprocess.run([sys.executable, "-c", _USER_CHILD, root, str(nstr), "1" if planck else "0",
-                    "1" if usrtau else "0", str(out), str(nwave)], check=True, env=env,
+                    "1" if usrtau else "0", str(out), str(nwave), "9"], check=True, env=env,
                    timeout=300)
     other = np.load(out)
     assert np.all(np.isfinite(here))
@@ -411,25 +415,28 @@ def test_many_user_angles_fallback_vs_oracle():
     assert margin(rel_err(flux, fref).max()) < TOL
 
 
-@pytest.mark.parametrize("nstr,planck,usrtau,nwave", [(16, False, False, 2), (16, True, True, 2),
-                                                      (8, True, False, 1), (12, False, True, 2),
-                                                      (4, True, True, 1)])
-def test_user_map_kernel_matches_direct(nstr, planck, usrtau, nwave, tmp_path):
+@pytest.mark.parametrize("nstr,planck,usrtau,nwave,nang", [
+    (16, False, False, 2, 9), (16, True, True, 2, 9), (8, True, False, 1, 9), (12, False, True, 2, 9),
+    (4, True, True, 1, 9), (16, False, True, 2, 8), (16, True, False, 1, 8), (10, True, True, 2, 8),
+    (16, True, True, 2, 4)])
+def test_user_map_kernel_matches_direct(nstr, planck, usrtau, nwave, nang, tmp_path):
     """nstr <= 16 user angles: the const kernel's per-(unit, layer) maps + the
     per-angle dot products (hd_rad_user_map_kernel, the default) against the
     per-angle Legendre sums, triangular solve and V^T products of
     hd_rad_user_kernel (HD_RAD_USER=direct, in a child process): the same
     integrals regrouped, to rounding -- level depths and caller depths inside
-    layers, beam and thermal sources, nine angles of both signs."""
+    layers, beam and thermal sources, nine angles of both signs.  Nine and eight
+    angles take the LDS-staged map kernel (four / eight units per wave, the last
+    wave partial), four angles the one it replaces."""
     import os
     import subprocess
     import sys
-    here = _user_case(nstr, planck, usrtau, nwave)
+    here = _user_case(nstr, planck, usrtau, nwave, nang)
     out = tmp_path / "direct.npy"
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, HD_AB="1", HD_RAD_USER="direct")
     subprocess.run([sys.executable, "-c", _USER_CHILD, root, str(nstr), "1" if planck else "0",
-                    "1" if usrtau else "0", str(out), str(nwave)], check=True, env=env,
+                    "1" if usrtau else "0", str(out), str(nwave), str(nang)], check=True, env=env,
                    timeout=300)
     other = np.load(out)
     assert np.all(np.isfinite(here))
