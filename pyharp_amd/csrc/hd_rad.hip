@@ -1388,6 +1388,10 @@ HD_RUNROLL
 #ifndef HD_RAD_UMAP_WAVES
 #define HD_RAD_UMAP_WAVES 2
 #endif
+#ifndef HD_RAD_UMAP_UTAU_REG
+#define HD_RAD_UMAP_UTAU_REG 1
+#endif
+constexpr bool kUmapUtauReg = HD_RAD_UMAP_UTAU_REG != 0;
 template <int NN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HD_RAD_UMAP_WAVES)))
 void hd_rad_user_map_kernel(RadArgs A) {
@@ -1448,6 +1452,10 @@ HD_RUNROLL
     if (A.planck) cur += A.planckv[(size_t)(L + 2) * A.ns + sl];
   }
   int k = up ? A.ntau - 1 : 0;
+  // the next user depth in ray order, held in a register: reloaded only when a depth
+  // is consumed, not on every layer's loop test (a dependent load per layer)
+  auto utau_at = [&](int kk) { return kk >= 0 && kk < A.ntau ? user_tau(A, kk, sl) : 0.0; };
+  double utk = kUmapUtauReg ? utau_at(k) : 0.0;
   double chk = 0.0;
   for (int step = 0; step < L; ++step) {
     const int lc = up ? L - 1 - step : step;
@@ -1544,12 +1552,14 @@ HD_RUNROLL
       return cin * exp(-fabs(tin - t) / anu) + integ(t, tin);
     };
     // the user depths in this layer, in ray order (one copy of the interior integral)
-    while (up ? (k >= 0 && user_tau(A, k, sl) >= ttop) : (k < A.ntau && user_tau(A, k, sl) <= tbot)) {
-      const double t = fmin(fmax((user_tau(A, k, sl) - ttop) * scale, 0.0), taup);
+    while (up ? (k >= 0 && (kUmapUtauReg ? utk : user_tau(A, k, sl)) >= ttop)
+              : (k < A.ntau && (kUmapUtauReg ? utk : user_tau(A, k, sl)) <= tbot)) {
+      const double t = fmin(fmax(((kUmapUtauReg ? utk : user_tau(A, k, sl)) - ttop) * scale, 0.0), taup);
       const double val = at(t);
       A.radm[((size_t)k * A.numu + iu) * nu + u] = val;
       chk += val;
       k += up ? -1 : 1;
+      if (kUmapUtauReg) utk = utau_at(k);
     }
     cur = cout;
   }
