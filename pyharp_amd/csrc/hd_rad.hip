@@ -1392,10 +1392,6 @@ HD_RUNROLL
 #define HD_RAD_UMAP_UTAU_REG 1
 #endif
 constexpr bool kUmapUtauReg = HD_RAD_UMAP_UTAU_REG != 0;
-#ifndef HD_RAD_UMAP_LAY_ILP
-#define HD_RAD_UMAP_LAY_ILP 1
-#endif
-constexpr int kUmapLayIlp = HD_RAD_UMAP_LAY_ILP;
 template <int NN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HD_RAD_UMAP_WAVES)))
 void hd_rad_user_map_kernel(RadArgs A) {
@@ -1534,7 +1530,7 @@ HD_RUNROLL
       const double reg = (1.0 - ek * emu) / fma(kk[j], anu, 1.0);
       const double sng = dexp(ek, emu, fma(-kk[j], anu, 1.0), lmu);
       lay = up ? fma(hpl[j], reg, fma(hmi[j], sng, lay)) : fma(hpl[j], sng, fma(hmi[j], reg, lay));
-      if ((j + 1) % kUmapLayIlp == 0) asm volatile("" : "+v"(lay));  // kUmapLayIlp eigen-terms' quotients and series at a time
+      asm volatile("" : "+v"(lay));  // one eigen-term's quotient and series at a time
     }
     if (beam) {
       const double e0l = rr[oE0 * HD_RS];
