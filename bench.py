@@ -416,7 +416,10 @@ def spawn_ranks(n: int, argv, env=None, program=None) -> int:
                 time.sleep(0.05)
     finally:
         # interrupted or terminated: no rank outlives this parent (they hold GPUs and
-        # would block the next run in a collective) -- SIGTERM, then SIGKILL after 10 s
+        # would block the next run in a collective) -- SIGTERM, then SIGKILL after 10 s.
+        # A second SIGTERM during this cleanup only records itself: raising again here
+        # would skip the SIGKILL escalation and leave ranks behind.
+        signal.signal(signal.SIGTERM, lambda signum, frame: None)
         for q in pending:
             if q.poll() is None:
                 q.send_signal(signal.SIGTERM)
@@ -427,7 +430,9 @@ def spawn_ranks(n: int, argv, env=None, program=None) -> int:
             except subprocess.TimeoutExpired:
                 q.kill()
                 q.wait()
-        signal.signal(signal.SIGTERM, old_term)
+        # None: the previous handler was not installed from Python -- leave ours
+        if old_term is not None:
+            signal.signal(signal.SIGTERM, old_term)
     return rc
 
 

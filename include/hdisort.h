@@ -134,9 +134,11 @@ int hd_context_get_timing(const hd_context *ctx, hd_timing *out);
  * have to grow during capture it returns HD_EINVAL instead. */
 int hd_context_reserve(hd_context *ctx, const hd_config *cfg, long nsolve);
 /* solves per internal chunk of an nsolve-solve call of this config under the automatic
- * chunking (hd_context_set_chunk 0): nstr <= 16 about 65 536 (one sweep wave per SIMD),
- * nstr 18..32 from a 16 GB scratch budget (about 16 000 at nlyr 80).  Chunk k+1's layer
- * kernel runs beside chunk k's sweep.  No device needed; -1 on bad args. */
+ * chunking (hd_context_set_chunk 0): nstr <= 16 about 32 768 when that gives five or
+ * more chunks, otherwise about 40 960 (a chunk's sweep leaves SIMDs to the next chunk's
+ * layer kernel), nstr 18..32 from a 16 GB scratch budget (about 16 000 at nlyr 80); a
+ * call that fits one chunk stays one.  Chunk k+1's layer kernel runs beside chunk k's
+ * sweep.  No device needed; -1 on bad args. */
 long hd_chunk_solves(const hd_config *cfg, long nsolve);
 
 /*

@@ -216,6 +216,16 @@ int ensure_rad_tables(hd_context* ctx) {
   return HD_OK;
 }
 
+constexpr long kRegChunkMax = 40960;  // the register path's largest automatic chunk
+
+// team path: bytes of scratch for the two chunks in flight (the per-solve size counts
+// both) within a 16 GB budget
+long team_chunk_target(int nn, int nlyr, bool planck) {
+  const double budget = 16.0 * 1024.0 * 1024.0 * 1024.0;
+  const double per = 8.0 * (double)hd::scratch_doubles_per_solve(nn, nlyr, planck);
+  return std::min<long>(262144, std::max<long>(16384, (long)(budget / per)));
+}
+
 long auto_chunk(long nsolve, int nn, int nlyr, bool planck) {
   // NN <= 8: the sweep runs one lane per solve at one wave per SIMD (its register
   // file is full) and cannot share a SIMD with the layer kernel.  Chunks of 32 000-
@@ -230,12 +240,9 @@ long auto_chunk(long nsolve, int nn, int nlyr, bool planck) {
   // (the rest of the 288 GB stays the caller's).
   long target;
   if (nn <= hd::kMaxRegNN) {
-    target = (nsolve + 32767) / 32768 >= 5 ? 32768 : 40960;
+    target = (nsolve + 32767) / 32768 >= 5 ? 32768 : kRegChunkMax;
   } else {
-    // bytes of scratch for the two chunks in flight (the per-solve size counts both)
-    const double budget = 16.0 * 1024.0 * 1024.0 * 1024.0;
-    const double per = 8.0 * (double)hd::scratch_doubles_per_solve(nn, nlyr, planck);
-    target = std::min<long>(262144, std::max<long>(16384, (long)(budget / per)));
+    target = team_chunk_target(nn, nlyr, planck);
   }
   // (team path: a call that fits one chunk stays one chunk.  Split in two, the 8-GPU
   // C5 rank shape -- 8 000 solves -- ran 1.155 M solves/s against 1.268 M: a 4 000-solve
@@ -244,6 +251,14 @@ long auto_chunk(long nsolve, int nn, int nlyr, bool planck) {
   if (nsolve <= target) return nsolve;
   const long n = (nsolve + target - 1) / target;
   return (nsolve + n - 1) / n;
+}
+
+// The largest chunk auto_chunk gives any call of at most nsolve solves (the chunk
+// size is not monotone in nsolve: 163 840 solves run in chunks of 32 768, 80 000 in
+// chunks of 40 000), so hd_context_reserve(nsolve) covers every smaller call too.
+long max_auto_chunk(long nsolve, int nn, int nlyr, bool planck) {
+  const long cap = nn <= hd::kMaxRegNN ? kRegChunkMax : team_chunk_target(nn, nlyr, planck);
+  return std::min(nsolve, cap);
 }
 
 // the last solve that used the context's buffers has finished (before a free)
@@ -520,7 +535,7 @@ int hd_context_reserve(hd_context* ctx, const hd_config* cfg, long nsolve) {
   HD_HIP(ctx, hipSetDevice(ctx->device));
   const bool planck_r = (cfg->flags & HD_FLAG_PLANCK) != 0;
   const long chunk = ctx->chunk > 0 ? std::min(ctx->chunk, nsolve)
-                                    : auto_chunk(nsolve, cfg->nstr / 2, cfg->nlyr, planck_r);
+                                    : max_auto_chunk(nsolve, cfg->nstr / 2, cfg->nlyr, planck_r);
   const size_t per = hd::scratch_doubles_per_solve(cfg->nstr / 2, cfg->nlyr,
                                                    (cfg->flags & HD_FLAG_PLANCK) != 0);
   // room for hd_solve_band's epilogue too, at its largest (any nwave): so a

@@ -279,8 +279,7 @@ __device__ __forceinline__ int layer_body(const LayerArgs& A, long s, int sl, in
       y2[i] = Qc.g[i] * rv;
       lxd[i] = Qc.sd[i] * xdi;
     }
-    lower_solve<NN>(lch, rdl, y2);
-    lower_t_solve<NN>(lch, rdl, y2);  // L^-T y2: V^T y2 = U^T L^-T y2 below
+    lower_solve<NN>(lch, rdl, y2);    // V^T y2 below (V = B K^-1 after the Jacobi)
     lower_solve<NN>(lch, rdl, lxd);   // lxd = L^-T L^-1 D^1/2 xd
     lower_t_solve<NN>(lch, rdl, lxd);
   } else {
@@ -310,27 +309,28 @@ __device__ __forceinline__ int layer_body(const LayerArgs& A, long s, int sl, in
   }
 
   // ---- eigenpairs (c_soleig): Sym = L^T (-A+) L = V diag(k^2) V^T ----
-  // With C C^T = -A+ (SPD exactly when Sym is), Sym = B^T B for B = C^T L: the
-  // one-sided Jacobi on B's columns gives k^2 = |b_j|^2 and B = B0 V, so
-  // U = L V = C^-T B comes from one triangular solve (it is all the beam and
-  // Omega need; V = L^-1 U only feeds Psi).  Sym itself is never formed.
+  // With C C^T = -A+ (SPD exactly when Sym is), X = L^T C has X X^T = Sym: the
+  // one-sided Jacobi on X's columns gives B = X W with orthogonal columns, and
+  // Sym B = X (X^T X) W = B diag(k^2), so k_j = |b_j| and V = B K^-1 directly --
+  // no triangular solve for the eigenvectors, and C is dead before the Jacobi.
+  // X^T X = C^T (-A-) C is closer to diagonal than B0^T B0 for B0 = X^T (the
+  // round-1..5 form): 4.0 instead of 4.8 sweeps per 64-lane wave at C4
+  // (per lane 3.76 vs 3.86; numpy model of this loop).
   double rdc[NN];
   if (!chol_inplace<NN>(ap, rdc)) st |= kStEigen;  // lower ap <- C
-  double v[NN][NN];  // B, then U = L V, then Omega = U Delta^1/2
+  double v[NN][NN];  // X, then B = X W, then Omega = L B K^-1 Delta^1/2
 #pragma unroll
   for (int i = 0; i < NN; ++i)
 #pragma unroll
-    for (int j = 0; j < NN; ++j) {  // B_ij = sum_{k >= max(i,j)} C_ki L_kj
+    for (int j = 0; j < NN; ++j) {  // X_ij = sum_{k >= max(i,j)} L_ki C_kj
       double t = 0.0;
 #pragma unroll
-      for (int k = (i > j ? i : j); k < NN; ++k) t = fma(ap[k][i], lch[k][j], t);
+      for (int k = (i > j ? i : j); k < NN; ++k) t = fma(lch[k][i], ap[k][j], t);
       v[i][j] = t;
     }
   // L is not needed again until the beam solution: park it in this lane's (not
-  // yet used) Psi staging area of LDS while B, C and the rotation temporaries
-  // hold the registers.  This keeps the kernel under 464 VGPR+AGPR, so that the
-  // previous chunk's 44-VGPR back-substitution waves still fit beside it on
-  // every SIMD (hd_solve's side stream).
+  // yet used) Psi staging area of LDS while B and the rotation temporaries hold
+  // the registers.
   constexpr int kPark = NN * (NN + 1) / 2 + NN;
   static_assert(kPark <= kPsi || NN == 1, "L does not fit the Psi staging area");
   if constexpr (NN > 1) {
@@ -346,23 +346,41 @@ __device__ __forceinline__ int layer_body(const LayerArgs& A, long s, int sl, in
   HD_PHASE();
   if (!jacobi_os<NN>(v, A.max_sweeps)) st |= kStEigen;
   HD_PHASE();
-  double kk[NN];
+  double kk[NN], rk[NN];  // k_j = |b_j|, 1/k_j
 #pragma unroll
   for (int j = 0; j < NN; ++j) {
     double k2 = 0.0;
 #pragma unroll
     for (int i = 0; i < NN; ++i) k2 = fma(v[i][j], v[i][j], k2);
     if (!(k2 > 0.0)) st |= kStEigen;
-    kk[j] = k2 > 0.0 ? k2 * rsq_nr1(k2) : 0.0;
+    const double r = k2 > 0.0 ? rsq_nr(k2) : 0.0;
+    kk[j] = k2 * r;
+    rk[j] = r;
   }
+  // beam, the part that needs only B and k (before L is back: y2 dies first)
+  double ybt[NN];  // B K^-1 tt, tt = V^T y2 / (1/mu0^2 - k^2), V = B K^-1
+  if (beam) {
+    double tt[NN];
+    const double r2 = rmu0 * rmu0;
 #pragma unroll
-  for (int j = 0; j < NN; ++j) {  // U = C^-T B, column by column
-    double x[NN];
+    for (int j = 0; j < NN; ++j) {
+      double t = 0.0;
 #pragma unroll
-    for (int i = 0; i < NN; ++i) x[i] = v[i][j];
-    lower_t_solve<NN>(ap, rdc, x);
+      for (int i = 0; i < NN; ++i) t = fma(v[i][j], y2[i], t);
+      double den = fma(-kk[j], kk[j], r2);
+      if (fabs(den) < 1.0e-9 * r2) {
+        st |= kStResonance;
+        den = den < 0.0 ? -1.0e-9 * r2 : 1.0e-9 * r2;
+      }
+      tt[j] = t * (rk[j] * rk[j]) * rcp_nr(den);  // K^-1 (V^T y2 / den)
+    }
 #pragma unroll
-    for (int i = 0; i < NN; ++i) v[i][j] = x[i];
+    for (int i = 0; i < NN; ++i) {
+      double t = 0.0;
+#pragma unroll
+      for (int j = 0; j < NN; ++j) t = fma(v[i][j], tt[j], t);
+      ybt[i] = t;
+    }
   }
   HD_PHASE();
   if constexpr (NN > 1) {  // L back from LDS
@@ -383,26 +401,12 @@ __device__ __forceinline__ int layer_body(const LayerArgs& A, long s, int sl, in
   double zp[NN], zm[NN];
   double e0 = 0.0;
   if (beam) {
-    double tt[NN];
-    const double r2 = rmu0 * rmu0;
-#pragma unroll
-    for (int j = 0; j < NN; ++j) {  // tt = V^T y2 / (1/mu0^2 - k^2)
-      double t = 0.0;
-#pragma unroll
-      for (int i = 0; i < NN; ++i) t = fma(v[i][j], y2[i], t);
-      double den = fma(-kk[j], kk[j], r2);
-      if (fabs(den) < 1.0e-9 * r2) {
-        st |= kStResonance;
-        den = den < 0.0 ? -1.0e-9 * r2 : 1.0e-9 * r2;
-      }
-      tt[j] = t * rcp_nr(den);
-    }
     double sv[NN], y[NN];
 #pragma unroll
-    for (int i = 0; i < NN; ++i) {  // s = W^-1 D^1/2 L V tt = W^-1 D^1/2 U tt
+    for (int i = NN - 1; i >= 0; --i) {  // s = W^-1 D^1/2 L V tt = W^-1 D^1/2 L (B K^-1 tt)
       double t = 0.0;
 #pragma unroll
-      for (int j = 0; j < NN; ++j) t = fma(v[i][j], tt[j], t);
+      for (int k = 0; k <= i; ++k) t = fma(lch[i][k], ybt[k], t);
       sv[i] = Qc.rg[i] * t;
     }
     // dd = (lxd - D^1/2 L^-T L^-1 D^1/2 (mu s) / mu0) / w
@@ -426,35 +430,46 @@ __device__ __forceinline__ int layer_body(const LayerArgs& A, long s, int sl, in
     for (int i = 0; i < NN; ++i) zp[i] = zm[i] = 0.0;
   }
 
+  HD_PHASE();
   // ---- layer operators in the flux-weighted basis ----
-  // Delta = tanh(k tau'/2)/k, Gamma = k tanh(k tau'/2)
-  double dsq[NN], gsq[NN];
+  // Delta = tanh(k tau'/2)/k, Gamma = k tanh(k tau'/2): Gamma^1/2 K^-1 = Delta^1/2
+  double dsq[NN];
 #pragma unroll
   for (int j = 0; j < NN; ++j) {
     const double x = kk[j] * taup;
     const double m = -expm1(-x);           // 1 - exp(-k tau')
     const double th = m * rcp_nr(2.0 - m);  // tanh(k tau'/2)
     const double delta = x > 1.0e-8 ? th * rcp_nr(kk[j] > 0.0 ? kk[j] : 1.0) : 0.5 * taup;
-    const double gg = kk[j] * th;
     dsq[j] = delta > 0.0 ? delta * rsq_nr1(delta) : 0.0;
-    gsq[j] = gg > 0.0 ? gg * rsq_nr1(gg) : 0.0;
   }
-  // Psi^T = L^-T V Gamma^1/2 = L^-T L^-1 U Gamma^1/2 -> LDS (one column per step)
+  // Psi^T = L^-T V Gamma^1/2 = L^-T B Delta^1/2 -> LDS (one column per step)
 #pragma unroll
   for (int j = 0; j < NN; ++j) {
     double x[NN];
 #pragma unroll
-    for (int i = 0; i < NN; ++i) x[i] = v[i][j];
-    lower_solve<NN>(lch, rdl, x);
+    for (int i = 0; i < NN; ++i) x[i] = v[i][j] * dsq[j];
     lower_t_solve<NN>(lch, rdl, x);
 #pragma unroll
-    for (int i = 0; i < NN; ++i) psi_lds[(i * NN + j) * kLayerBlock + lt] = x[i] * gsq[j];
+    for (int i = 0; i < NN; ++i) psi_lds[(i * NN + j) * kLayerBlock + lt] = x[i];
   }
-  // Omega = L V Delta^1/2 = U Delta^1/2, in place over v
+  HD_PHASE();
+  // Omega = U Delta^1/2 = L B K^-1 Delta^1/2, in place over v (rows bottom-up)
 #pragma unroll
-  for (int i = 0; i < NN; ++i)
+  for (int j = 0; j < NN; ++j) {
+    const double sc = rk[j] * dsq[j];
 #pragma unroll
-    for (int j = 0; j < NN; ++j) v[i][j] *= dsq[j];
+    for (int i = 0; i < NN; ++i) v[i][j] *= sc;
+  }
+#pragma unroll
+  for (int i = NN - 1; i >= 0; --i)
+#pragma unroll
+    for (int j = 0; j < NN; ++j) {
+      double t = 0.0;
+#pragma unroll
+      for (int k = 0; k <= i; ++k) t = fma(lch[i][k], v[k][j], t);
+      v[i][j] = t;
+    }
+  HD_PHASE();
 
   using RL = RecL<NN>;
   constexpr int nsym = NN * (NN + 1) / 2;

@@ -8,9 +8,9 @@ never imported by the product.
 Formulation:
   * homogeneous solution from the symmetrised eigenproblem
       L L^T = D^1/2 (W^-1 - S-) D^1/2,   C C^T = D^1/2 (W^-1 - S+) D^1/2,
-      Sym = L^T C C^T L = B0^T B0 with B0 = C^T L;  the kernel's one-sided
-    Jacobi rotates B0's columns into B = B0 V, so k^2 = |b_j|^2 and
-    U = L V = C^-T B (here V comes from eigh of B0^T B0)
+      Sym = L^T C C^T L = X X^T with X = L^T C;  the kernel's one-sided
+    Jacobi rotates X's columns into B = X W (orthogonal columns), so
+    k^2 = |b_j|^2, V = B K^-1 and U = L V (here V comes from eigh of X X^T)
   * layer operators in the flux-weighted basis, Omega = U Delta^1/2,
     Psi^T = L^-T V Gamma^1/2, and by Woodbury
       A- = (I + Omega Omega^T)^-1, A+ = (I + Psi^T Psi)^-1,
@@ -47,15 +47,15 @@ def layer_ops(dtau, ssa, chi, nstr, umu0, fbeam, b_top, b_bot, tauc_top):
     am = np.diag(1.0 / mu) - sd[:, None] * sminus * sd[None, :]
     ap = np.diag(1.0 / mu) - sd[:, None] * splus * sd[None, :]
     lch = np.linalg.cholesky(am)
-    # one-sided Jacobi view (hd_layer_kernel): C C^T = -A+, B0 = C^T L, Sym = B0^T B0;
-    # the rotations give B = B0 V with k^2 = |b_j|^2, and U = L V = C^-T B
+    # one-sided Jacobi view (hd_layer_kernel): C C^T = -A+, X = L^T C, Sym = X X^T;
+    # the rotations give B = X W with k^2 = |b_j|^2, V = B K^-1 and U = L V
     cch = np.linalg.cholesky(ap)
-    b0 = cch.T @ lch
-    k2, v = np.linalg.eigh(b0.T @ b0)
-    bcols = b0 @ v
+    x = lch.T @ cch
+    _, wv = np.linalg.eigh(x.T @ x)
+    bcols = x @ wv
     k2 = np.sum(bcols * bcols, axis=0)
     k = np.sqrt(k2)
-    u = np.linalg.solve(cch.T, bcols)         # U = L V = C^-T B
+    u = lch @ (bcols / k[None, :])            # U = L V = L B K^-1
     # ---- layer operators in the flux-weighted basis (g = sqrt(w mu)) ----
     e = np.exp(-k * taup)
     m = -np.expm1(-k * taup)

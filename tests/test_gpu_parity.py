@@ -722,3 +722,56 @@ def test_reserve_then_capture_band(nstr):
         raise res["error"]
     assert "inside a stream capture" in res.get("refused", ""), res.get("refused")
     assert torch.equal(res["replay"], res["eager"])
+
+
+def test_reserve_covers_smaller_calls():
+    """hd_context_reserve(N) covers every call of at most N solves: the automatic
+    chunk is not monotone in the call size (640 000 solves run in chunks of 32 000,
+    80 000 in chunks of 40 000), so a reserve of the C4 shape must size for the
+    largest chunk a smaller call can get.  On a fresh context (a new host thread's),
+    reserve(640 000) and then capture an 80 000-solve fused band solve: it must not
+    need to grow scratch, and the replay equals the eager result bit for bit."""
+    import threading
+    from pyharp_amd import _lib
+    from pyharp_amd.disort import _context
+    rng = np.random.default_rng(61)
+    nstr, nwave, ncol, nlyr = 4, 8, 10000, 3
+    cfg = _lib.HdConfig(nstr=nstr, nmom=nstr, nlyr=nlyr, nprop=2 + nstr,
+                        flags=_lib.HD_FLAG_LAMBER | _lib.HD_FLAG_ONLYFL)
+    assert _lib.chunk_solves(nstr, nlyr, 640000) == 32000
+    assert _lib.chunk_solves(nstr, nlyr, nwave * ncol) == 40000
+    prop, bc, _ = _random_batch(rng, nwave, ncol, nlyr, nstr, False)
+    dev = torch.device("cuda", 0)
+    p = torch.as_tensor(prop, device=dev)
+    b = {k: torch.as_tensor(v, device=dev) for k, v in bc.items()}
+    w = torch.as_tensor(rng.uniform(0.1, 1.0, nwave), device=dev)
+    res = {}
+
+    def worker():
+        try:
+            _context(0).reserve(cfg, 640000)
+            d = _disort(nstr, nlyr, nwave, ncol)
+            st = torch.zeros(nwave * ncol, dtype=torch.int32, device=dev)
+            out = torch.empty((ncol, nlyr + 1, 2), dtype=torch.float64, device=dev)
+            s = torch.cuda.Stream(device=dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s):
+                    d.forward_band(p, b, weights=w, out=out, status=st)
+            out.zero_()
+            g.replay()
+            torch.cuda.synchronize()
+            res["replay"] = out.clone()
+            res["eager"] = d.forward_band(p, b, weights=w)
+            torch.cuda.synchronize()
+        except BaseException as e:  # surfaced in the main thread
+            res["error"] = e
+
+    t = threading.Thread(target=worker)
+    t.start()
+    t.join(timeout=100)
+    assert not t.is_alive()
+    if "error" in res:
+        raise res["error"]
+    assert torch.equal(res["replay"], res["eager"])

@@ -425,9 +425,9 @@ def test_user_map_kernel_matches_direct(nstr, planck, usrtau, nwave, nang, tmp_p
     per-angle Legendre sums, triangular solve and V^T products of
     hd_rad_user_kernel (HD_RAD_USER=direct, in a child process): the same
     integrals regrouped, to rounding -- level depths and caller depths inside
-    layers, beam and thermal sources, nine angles of both signs.  Nine and eight
-    angles take the LDS-staged map kernel (four / eight units per wave, the last
-    wave partial), four angles the one it replaces."""
+    layers, beam and thermal sources, nine angles of both signs.  Every angle count
+    runs the one map kernel (hd_rad_user_map_kernel); the eight- and four-angle cases
+    exercise its partial waves."""
     import os
     import subprocess
     import sys
