@@ -423,10 +423,12 @@ int hd_context_create(hd_context** out, int device) {
                 ndev);
   hd_context* ctx = new hd_context();
   if (const char* e = hd::ab_env("HD_JACOBI_WARM")) ctx->warm = std::atoi(e) != 0;
-  if (const char* e = hd::ab_env("HD_TEAM_SWEEP_LEAN")) ctx->lean = std::atoi(e) != 0;
   if (const char* e = hd::ab_env("HD_SWEEP_QUAD")) ctx->quad = std::atoi(e) < 0 ? -1 : std::atoi(e) != 0;
+#if HD_AB_VARIANTS
+  if (const char* e = hd::ab_env("HD_TEAM_SWEEP_LEAN")) ctx->lean = std::atoi(e) != 0;
   if (const char* e = hd::ab_env("HD_SWEEP_LEAN8")) ctx->lean8 = std::atoi(e) != 0;
   if (const char* e = hd::ab_env("HD_COLUMN")) ctx->column = std::atoi(e) != 0;
+#endif
   ctx->device = device;
   auto init = [ctx]() -> int {
     HD_HIP(ctx, hipSetDevice(ctx->device));

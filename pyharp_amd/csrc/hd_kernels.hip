@@ -907,6 +907,7 @@ __global__ __launch_bounds__(64) void hd_sweep_kernel(SweepArgs A) {
 template <int NN, bool PRE, bool NT>
 __device__ __forceinline__ void backsub_body(const SweepArgs& A);
 
+#if HD_AB_VARIANTS
 // ============================================================================
 // K1+K2+K3 in one pass per solve (the column kernel): one lane walks its solve's
 // layers top -> bottom, runs each layer's setup (layer_body) into registers and
@@ -1295,6 +1296,8 @@ void hd_sweep_lean_kernel(SweepArgs A) {
     if (st & 0x0F) atomicOr(A.anyerr, 1);
   }
 }
+
+#endif  // HD_AB_VARIANTS
 
 // ============================================================================
 // K2 for nstr 4 and 8 (NN = 2, 4) in NN-lane teams: the adding sweep of
@@ -1870,6 +1873,7 @@ static void launch_sweep(const SweepArgs& sa, hipStream_t stream) {
       return;
     }
   }
+#if HD_AB_VARIANTS
   if constexpr (NN == 8) {
     if (sa.lean8) {
       hipLaunchKernelGGL(hd_sweep_lean_kernel<NN>, dim3((unsigned)((sa.nsc + 63) / 64)), dim3(64),
@@ -1877,6 +1881,7 @@ static void launch_sweep(const SweepArgs& sa, hipStream_t stream) {
       return;
     }
   }
+#endif
   if (sa.nsc >= kNtMinSolves)
     hipLaunchKernelGGL((hd_sweep_kernel<NN, true>), dim3((unsigned)((sa.nsc + 63) / 64)), dim3(64),
                        0, stream, sa);
@@ -1968,12 +1973,17 @@ hipError_t launch_layer_nn(int nn, const LayerArgs& la, hipStream_t stream) {
   return hipGetLastError();
 }
 hipError_t launch_column_nn(int nn, const LayerArgs& la, const SweepArgs& sa, hipStream_t stream) {
+#if HD_AB_VARIANTS
   const dim3 grid((unsigned)((sa.nsc + 63) / 64)), block(64);
   switch (nn) {
     case 8: hipLaunchKernelGGL(hd_column_kernel<8>, grid, block, 0, stream, la, sa); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+#else
+  (void)nn, (void)la, (void)sa, (void)stream;
+  return hipErrorInvalidValue;  // A/B build only
+#endif
 }
 
 hipError_t launch_sweep_nn(int nn, const SweepArgs& sa, hipStream_t stream) {

@@ -302,6 +302,14 @@ inline int band_steps(int nwave) {
   while ((1 << k) < (nwave < 64 ? nwave : 64)) ++k;
   return k;
 }
+// Kernel variants that were measured and not kept (the column
+// kernel, the LDS-state nstr-16 sweep, the one-wave team sweep, the VALU team layer
+// and sweep kernels, the per-angle radiance user kernel at nstr <= 16) are compiled
+// only into the A/B build (scripts/ab/build_variant.sh defines HD_AB_VARIANTS=1):
+// the product library carries only the kernels its dispatch can select.
+#ifndef HD_AB_VARIANTS
+#define HD_AB_VARIANTS 0
+#endif
 // A/B switches of the kernel variants (HD_JACOBI_WARM, HD_TEAM_SWEEP_LEAN, HD_SWEEP_QUAD,
 // HD_SWEEP_LEAN8, HD_RAD_USER, HD_TEAM_LAYER, HD_TEAM_SWEEP) are read only when the
 // single opt-in HD_AB=1 is set too: a stray variable in a user's environment never

@@ -1843,11 +1843,15 @@ static bool rad_user_rolled() {
 
 // HD_RAD_USER=direct: nstr <= 16 user angles by the per-angle hd_rad_user_kernel
 static bool rad_user_direct() {
+#if HD_AB_VARIANTS
   static const bool v = [] {
     const char* e = ab_env("HD_RAD_USER");
     return e && std::strcmp(e, "direct") == 0;
   }();
   return v;
+#else
+  return false;  // the per-angle kernel at nstr <= 16: A/B build only
+#endif
 }
 
 template <int NN>
@@ -1894,9 +1898,11 @@ static void launch_rad(const RadArgs& a, bool radiances, hipStream_t st) {
                          dim3(64), 0, st, ac);
     else
 #endif
-    if (!team_user)
-      hipLaunchKernelGGL(hd_rad_user_kernel<NN>, dim3((unsigned)((nr + 63) / 64), (unsigned)a.nm),
-                         dim3(64), 0, st, a);
+    if constexpr (NN > kMaxRegNN || HD_AB_VARIANTS) {
+      if (!team_user)
+        hipLaunchKernelGGL(hd_rad_user_kernel<NN>, dim3((unsigned)((nr + 63) / 64), (unsigned)a.nm),
+                           dim3(64), 0, st, a);
+    }
     const long na = (long)a.ns * a.nphi * a.ntau * a.numu;
     hipLaunchKernelGGL(hd_rad_azimuth_kernel, dim3((unsigned)((na + 255) / 256)), dim3(256), 0,
                        st, a);

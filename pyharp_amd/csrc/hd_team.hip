@@ -38,6 +38,7 @@ __constant__ QuadTablesTeam c_quad_team;
 
 using namespace team;
 
+#if HD_AB_VARIANTS  // the VALU team kernels: A/B build only (the product runs hd_team_mfma.hip)
 // ============================================================================
 // K1 (team): per-(solve, layer) setup
 // ============================================================================
@@ -542,6 +543,8 @@ __global__ __launch_bounds__(kTeamBlock) void hd_team_sweep_kernel(SweepArgs A) 
   }
 }
 
+#endif  // HD_AB_VARIANTS
+
 // ============================================================================
 // host side
 // ============================================================================
@@ -580,21 +583,29 @@ hipError_t upload_quad_tables_team(const QuadHost* per_nn /* [kMaxNN], index nn-
 // HD_TEAM_LAYER=valu selects the VALU-product layer kernel (A/B runs); the
 // default is the MFMA one (hd_team_mfma.hip)
 static bool team_layer_valu() {
+#if HD_AB_VARIANTS
   static const bool v = [] {
     const char* e = ab_env("HD_TEAM_LAYER");
     return e && std::strcmp(e, "valu") == 0;
   }();
   return v;
+#else
+  return false;
+#endif
 }
 
 // HD_TEAM_SWEEP=valu selects the VALU-product sweep (A/B runs); the default is
 // the MFMA one (hd_team_mfma.hip)
 static bool team_sweep_valu() {
+#if HD_AB_VARIANTS
   static const bool v = [] {
     const char* e = ab_env("HD_TEAM_SWEEP");
     return e && std::strcmp(e, "valu") == 0;
   }();
   return v;
+#else
+  return false;
+#endif
 }
 
 template <int NN>
@@ -608,7 +619,9 @@ static hipError_t launch_team(const PlanckArgs* pa, const TaucArgs* ta, const La
   // timing quadruple: layer start / end, sweep start / end
   if (ev) (void)hipEventRecord(ev[0], stream);
   if (team_layer_valu()) {
+#if HD_AB_VARIANTS
     hipLaunchKernelGGL(hd_team_layer_kernel<NN>, dim3(nb1), dim3(kTeamBlock), 0, stream, la);
+#endif
   } else {
     const hipError_t e = launch_team_layer_mfma(NN, la, stream);
     if (e != hipSuccess) return e;
@@ -620,7 +633,11 @@ static hipError_t launch_team(const PlanckArgs* pa, const TaucArgs* ta, const La
     if (ev) (void)hipEventRecord(ev[3], stream);
     return e;
   }
+#if HD_AB_VARIANTS
   hipLaunchKernelGGL(hd_team_sweep_kernel<NN>, dim3(nb2), dim3(kTeamBlock), 0, stream, sa);
+#else
+  (void)nb2;
+#endif
   if (ev) (void)hipEventRecord(ev[3], stream);
   return hipGetLastError();
 }
@@ -629,19 +646,23 @@ static hipError_t launch_team(const PlanckArgs* pa, const TaucArgs* ta, const La
 // (chunk k+1's layer kernel on one stream beside chunk k's sweep on another)
 template <int NN>
 static hipError_t launch_team_layer(const LayerArgs& la, hipStream_t stream) {
+#if HD_AB_VARIANTS
   if (team_layer_valu()) {
     const long nt1 = (long)la.nsc * la.nlyr;
     const unsigned nb1 = (unsigned)((nt1 + kTeamsPerBlock - 1) / kTeamsPerBlock);
     hipLaunchKernelGGL(hd_team_layer_kernel<NN>, dim3(nb1), dim3(kTeamBlock), 0, stream, la);
     return hipGetLastError();
   }
+#endif
   return launch_team_layer_mfma(NN, la, stream);
 }
 template <int NN>
 static hipError_t launch_team_sweep(const SweepArgs& sa, hipStream_t stream) {
   if (!team_sweep_valu()) return launch_team_sweep_mfma(NN, sa, stream);
+#if HD_AB_VARIANTS
   const unsigned nb2 = (unsigned)((sa.nsc + kTeamsPerBlock - 1) / kTeamsPerBlock);
   hipLaunchKernelGGL(hd_team_sweep_kernel<NN>, dim3(nb2), dim3(kTeamBlock), 0, stream, sa);
+#endif
   return hipGetLastError();
 }
 

@@ -563,6 +563,7 @@ __global__ __launch_bounds__(64, 2) void hd_team_mfma_layer_kernel(LayerArgs A) 
   }
 }
 
+#if HD_AB_VARIANTS  // the one-wave team sweep: A/B build only (the product runs the lean one)
 // ============================================================================
 // K2 (team, MFMA): adding sweep + back-substitution, four solves per wave.
 // The register/team sweep's update per layer
@@ -834,8 +835,7 @@ __global__ __launch_bounds__(64, 1) void hd_team_mfma_sweep_kernel(SweepArgs A) 
     if (st & 0x0F) atomicOr(A.anyerr, 1);
   }
 }
-
-
+#endif  // HD_AB_VARIANTS
 
 // ============================================================================
 // K2 (team, MFMA), lean: the same sweep and back-substitution as
@@ -1840,9 +1840,11 @@ static hipError_t launch_sweep(const SweepArgs& sa, hipStream_t stream) {
     hipLaunchKernelGGL((hd_team_mfma_sweep_lean_kernel<NN, true>), gl, dim3(64), 0, stream, sa);
   else if (sa.lean)
     hipLaunchKernelGGL((hd_team_mfma_sweep_lean_kernel<NN, false>), gl, dim3(64), 0, stream, sa);
+#if HD_AB_VARIANTS
   else
     hipLaunchKernelGGL(hd_team_mfma_sweep_kernel<NN>, dim3((unsigned)((sa.nsc + 3) / 4)), dim3(64),
                        0, stream, sa);
+#endif
   return hipGetLastError();
 }
 

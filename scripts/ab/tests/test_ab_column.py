@@ -15,13 +15,15 @@ import sys
 import numpy as np
 import pytest
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(HERE)))
 pytestmark = pytest.mark.gpu
 
 CHILD = r"""
 import sys, numpy as np
 sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + '/tests')
-from test_gpu_column import _solve
+sys.path.insert(0, sys.argv[1] + '/scripts/ab/tests')
+from test_ab_column import _solve
 f, b = _solve(sys.argv[2] == '1')
 np.save(sys.argv[3], f); np.save(sys.argv[4], b)
 """
@@ -53,11 +55,11 @@ def _solve(planck):
 
 
 @pytest.mark.parametrize("planck", [False, True])
-def test_column_kernel_matches_three_kernel_path(planck, tmp_path):
+def test_column_kernel_matches_three_kernel_path(planck, tmp_path, ab_lib):
     here_f, here_b = _solve(planck)
     col_here = os.environ.get("HD_AB") == "1" and os.environ.get("HD_COLUMN") == "1"
     of, ob = tmp_path / "f.npy", tmp_path / "b.npy"
-    env = dict(os.environ, HD_AB="1", HD_COLUMN="0" if col_here else "1")
+    env = dict(os.environ, HD_LIB_PATH=ab_lib, HD_AB="1", HD_COLUMN="0" if col_here else "1")
     subprocess.run([sys.executable, "-c", CHILD, ROOT, "1" if planck else "0", str(of), str(ob)],
                    check=True, env=env, timeout=300)
     other_f, other_b = np.load(of), np.load(ob)

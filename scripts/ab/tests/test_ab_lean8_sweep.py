@@ -13,13 +13,15 @@ import sys
 import numpy as np
 import pytest
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(HERE)))
 pytestmark = pytest.mark.gpu
 
 CHILD = r"""
 import sys, numpy as np
 sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + '/tests')
-from test_gpu_lean8_sweep import _solve
+sys.path.insert(0, sys.argv[1] + '/scripts/ab/tests')
+from test_ab_lean8_sweep import _solve
 np.save(sys.argv[3], _solve(sys.argv[2] == '1'))
 """
 
@@ -43,11 +45,11 @@ def _solve(planck, chunk=23):
 
 
 @pytest.mark.parametrize("planck", [False, True])
-def test_lean8_sweep_matches_register_sweep(planck, tmp_path):
+def test_lean8_sweep_matches_register_sweep(planck, tmp_path, ab_lib):
     here = _solve(planck)
     lean_here = os.environ.get("HD_AB") == "1" and os.environ.get("HD_SWEEP_LEAN8") == "1"
     out = tmp_path / "other.npy"
-    env = dict(os.environ, HD_AB="1", HD_SWEEP_LEAN8="0" if lean_here else "1")
+    env = dict(os.environ, HD_LIB_PATH=ab_lib, HD_AB="1", HD_SWEEP_LEAN8="0" if lean_here else "1")
     subprocess.run([sys.executable, "-c", CHILD, ROOT, "1" if planck else "0", str(out)],
                    check=True, env=env, timeout=300)
     other = np.load(out)

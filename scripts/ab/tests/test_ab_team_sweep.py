@@ -11,13 +11,15 @@ import sys
 import numpy as np
 import pytest
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(HERE)))
 pytestmark = pytest.mark.gpu
 
 CHILD = r"""
 import sys, numpy as np
 sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + '/tests')
-from test_gpu_lean_sweep import _solve
+sys.path.insert(0, sys.argv[1] + '/scripts/ab/tests')
+from test_ab_team_sweep import _solve
 np.save(sys.argv[4], _solve(int(sys.argv[2]), sys.argv[3] == '1'))
 """
 
@@ -41,11 +43,11 @@ def _solve(nstr, planck, chunk=23):
 
 
 @pytest.mark.parametrize("nstr,planck", [(18, False), (24, True), (32, False), (32, True)])
-def test_lean_sweep_bitwise(nstr, planck, tmp_path):
+def test_lean_sweep_bitwise(nstr, planck, tmp_path, ab_lib):
     here = _solve(nstr, planck)
     lean_here = not (os.environ.get("HD_AB") == "1" and os.environ.get("HD_TEAM_SWEEP_LEAN") == "0")
     out = tmp_path / "other.npy"
-    env = dict(os.environ, HD_AB="1", HD_TEAM_SWEEP_LEAN="0" if lean_here else "1")
+    env = dict(os.environ, HD_LIB_PATH=ab_lib, HD_AB="1", HD_TEAM_SWEEP_LEAN="0" if lean_here else "1")
     subprocess.run([sys.executable, "-c", CHILD, ROOT, str(nstr), "1" if planck else "0",
                     str(out)], check=True, env=env, timeout=300)
     other = np.load(out)

@@ -5,6 +5,8 @@
 # call (nothing more touches the GPU after a failed step).  Outputs: gpurun_out/TAG/.
 #   tests[=SEL[@K]]      pytest -m gpu in one process (SEL: comma-separated selectors,
 #                        K: a -k expression with '+' for spaces)
+#   abtests              pytest -m gpu scripts/ab/tests (the not-kept variants, on
+#                        ab_libs/libhdisort_ab.so: build it first, scripts/ab/build_variant.sh ab)
 #   smoke                __graft_entry__.smoke()
 #   bench=NAME[:ARGS]    python bench.py ARGS              > bench_NAME.json
 #   stats=NAME[:ARGS]    rocprofv3 --kernel-trace --stats of bench.py ARGS:
@@ -49,6 +51,11 @@ for step in "$@"; do
       HD_MARGINS_OUT=$OUT/parity_margins.json timeout -k 10 840 python -u -m pytest $sel -m gpu ${kexpr:+-k "$kexpr"} -x -v --timeout 120 \
         --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || { tail -40 "$OUT/pytest_gpu.log"; exit 1; }
       tail -3 "$OUT/pytest_gpu.log" ;;
+    abtests)
+      say "pytest -m gpu scripts/ab/tests"
+      timeout -k 10 600 python -u -m pytest scripts/ab/tests -m gpu -x -v --timeout 300 \
+        --timeout-method thread > "$OUT/pytest_ab.log" 2>&1 || { tail -40 "$OUT/pytest_ab.log"; exit 1; }
+      tail -3 "$OUT/pytest_ab.log" ;;
     smoke)
       say smoke
       timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
