@@ -355,12 +355,21 @@ HD_UNROLL_NN
 // columns -- against 2(NN-2) + 2 NN mul/fma pairs for the two-sided update of
 // Sym and V.  Same tournament ordering and parameter formulas as jacobi_round.
 // ----------------------------------------------------------------------------
+// Column scales: b_j = sg_j x_j (x is what the registers hold), so the rotation
+//   b_p' = c (b_p - t b_q),  b_q' = c (b_q + t b_p)
+// becomes  x_p' = x_p - (t sg_q / sg_p) x_q,  x_q' = x_q + (t sg_p / sg_q) x_p,
+// sg' = c sg: one FMA per element instead of a MUL and an FMA (rs = 1/sg is
+// carried beside sg; 1/c = (1 + t^2) c).  The tracked norms |b_p|^2, |b_q|^2 move
+// by -/+ t (b_p.b_q) -- the two-sided Jacobi diagonal update, exact at the exact
+// angle and stationary in t there, so the FP32 angle's error only enters at second
+// order; the norms are recomputed from the columns at every sweep start anyway.
 template <int NN>
 __device__ __forceinline__ void jacobi_os_round(int r, double (&b)[NN][NN], double (&nrm)[NN],
-                                                bool on, double& off) {
+                                                double (&sg)[NN], double (&rs)[NN], bool on,
+                                                double& off) {
   constexpr int P = NN + (NN & 1);
   constexpr int H = P / 2;
-  double cc[H], ss[H], gg[H];
+  double tt[H], cc[H], gg[H];
 HD_UNROLL_NN
   for (int k = 0; k < H; ++k) {
     const int x = tour_a(P, r, k), y = tour_b(P, r, k);
@@ -372,7 +381,7 @@ HD_UNROLL_NN
       if (i % 2 == 0) g0 = fma(b[i][p], b[i][q], g0);
       else g1 = fma(b[i][p], b[i][q], g1);
     }
-    const double gam = g0 + g1;
+    const double gam = (g0 + g1) * (sg[p] * sg[q]);
     const double app = nrm[p], aqq = nrm[q];
     const double g2 = gam * gam;
     off += g2;
@@ -380,27 +389,22 @@ HD_UNROLL_NN
     const double d = aqq - app;
 #if HD_JACOBI_F32_ANGLE
     // The angle in FP32, t = tan(theta) = sgn(d) 2 g / (|d| + sqrt(d^2 + 4 g^2));
-    // c = 1/sqrt(1 + t^2) and s = t c in FP64, so the rotation is orthogonal to FP64
-    // rounding whatever t is: an angle good to ~1e-7 only leaves ~1e-7 of g behind,
-    // which the next sweep removes (quadratic convergence until off ~ 1e-7 of the
+    // c = 1/sqrt(1 + t^2) in FP64, so the rotation is orthogonal to FP64 rounding
+    // whatever t is: an angle good to ~1e-7 only leaves ~1e-7 of g behind, which
+    // the next sweep removes (quadratic convergence until off ~ 1e-7 of the
     // diagonal; the stop rule sits at 1e-8)
     const float df = (float)d, g2f = 2.0f * (float)gam;
     const float wf = __builtin_amdgcn_sqrtf(__builtin_fmaf(g2f, g2f, df * df));
     const float tf = (df < 0.0f ? -g2f : g2f) * __builtin_amdgcn_rcpf(__builtin_fabsf(df) + wf);
     const double t = rot ? (double)tf : 0.0;
-    const double c = rsq_nr1(fma(t, t, 1.0));  // exactly 1 for t = 0
-    cc[k] = c;
-    ss[k] = t * c;
 #else
-    // w = sqrt(d^2 + 4 g^2), u = |d| + w, z = 1/sqrt(2 w u): c = u z, s = sgn(d) 2 g z
+    // w = sqrt(d^2 + 4 g^2): t = sgn(d) 2 g / (|d| + w)
     const double w2 = rot ? fma(d, d, 4.0 * g2) : 1.0;
     const double w = w2 * rsq_nr1(w2);
-    const double u = fabs(d) + w;
-    const double z = rsq_nr1(2.0 * w * u);
-    const double sg = d < 0.0 ? -2.0 : 2.0;
-    cc[k] = rot ? u * z : 1.0;
-    ss[k] = rot ? sg * gam * z : 0.0;
+    const double t = rot ? (d < 0.0 ? -2.0 : 2.0) * gam * rcp_nr(fabs(d) + w) : 0.0;
 #endif
+    tt[k] = t;
+    cc[k] = rsq_nr1(fma(t, t, 1.0));  // exactly 1 for t = 0
     gg[k] = gam;
   }
 HD_UNROLL_NN
@@ -408,18 +412,21 @@ HD_UNROLL_NN
     const int x = tour_a(P, r, k), y = tour_b(P, r, k);
     const int p = x < y ? x : y, q = x < y ? y : x;
     if (q >= NN) continue;
-    const double c = cc[k], s = ss[k];
+    const double t = tt[k], c = cc[k];
+    const double al = -t * (sg[q] * rs[p]), be = t * (sg[p] * rs[q]);
 HD_UNROLL_NN
     for (int i = 0; i < NN; ++i) {
       const double bp = b[i][p], bq = b[i][q];
-      b[i][p] = fma(-s, bq, c * bp);
-      b[i][q] = fma(s, bp, c * bq);
+      b[i][p] = fma(al, bq, bp);
+      b[i][q] = fma(be, bp, bq);
     }
-    // |c b_p - s b_q|^2 and |s b_p + c b_q|^2
-    const double app = nrm[p], aqq = nrm[q];
-    const double c2 = c * c, s2 = s * s, cs2 = 2.0 * c * s * gg[k];
-    nrm[p] = fma(c2, app, fma(s2, aqq, -cs2));
-    nrm[q] = fma(s2, app, fma(c2, aqq, cs2));
+    const double rc = fma(t, t, 1.0) * c;  // 1/c
+    sg[p] *= c;
+    sg[q] *= c;
+    rs[p] *= rc;
+    rs[q] *= rc;
+    nrm[p] = fma(-t, gg[k], nrm[p]);
+    nrm[q] = fma(t, gg[k], nrm[q]);
   }
 }
 
@@ -427,16 +434,20 @@ HD_UNROLL_NN
 // (accumulated from the pairs' b_p.b_q as they were rotated) stayed below
 // 1e-8 of its diagonal: quadratic convergence leaves ~1e-16 after it (the
 // criterion of jacobi_eig, measured one sweep earlier).  A converged lane stops
-// rotating (exact no-ops: c = 1, s = 0), so its result does not depend on which
-// solves share its wave; the loop exits when every lane has converged.  Returns
-// false when this lane left at max_sweeps still rotating (not converged: the
-// caller sets the EIGEN status bit).
+// rotating (exact no-ops: t = 0), so its result does not depend on which
+// solves share its wave; the loop exits when every lane has converged.  The
+// column scales are folded back into b at the end.  Returns false when this lane
+// left at max_sweeps still rotating (not converged: the caller sets the EIGEN
+// status bit).
 template <int NN>
 __device__ __forceinline__ bool jacobi_os(double (&b)[NN][NN], int max_sweeps) {
   bool on = false;
   if constexpr (NN > 1) {
     constexpr int P = NN + (NN & 1);
     on = true;
+    double sg[NN], rs[NN];
+HD_UNROLL_NN
+    for (int j = 0; j < NN; ++j) sg[j] = rs[j] = 1.0;
     for (int sweep = 0; sweep < max_sweeps; ++sweep) {
       double nrm[NN], dia = 0.0, off = 0.0;
 HD_UNROLL_NN
@@ -444,14 +455,18 @@ HD_UNROLL_NN
         double t = 0.0;
 HD_UNROLL_NN
         for (int i = 0; i < NN; ++i) t = fma(b[i][j], b[i][j], t);
-        nrm[j] = t;
-        dia = fma(t, t, dia);
+        nrm[j] = t * (sg[j] * sg[j]);
+        dia = fma(nrm[j], nrm[j], dia);
       }
 HD_UNROLL_NN
-      for (int r = 0; r < P - 1; ++r) jacobi_os_round<NN>(r, b, nrm, on, off);
+      for (int r = 0; r < P - 1; ++r) jacobi_os_round<NN>(r, b, nrm, sg, rs, on, off);
       on = on && off > 1.0e-16 * dia;
       if (__all(!on)) break;
     }
+HD_UNROLL_NN
+    for (int j = 0; j < NN; ++j)
+HD_UNROLL_NN
+      for (int i = 0; i < NN; ++i) b[i][j] *= sg[j];
   }
   return !on;
 }

@@ -197,29 +197,6 @@ __device__ __forceinline__ void team_tri_inverse_col(double (&jr)[NN], double& j
   });
 }
 
-// team_tri_inverse_col of two independent factors in lockstep (interleaved chains)
-template <int NN>
-__device__ __forceinline__ void team_tri_inverse_col2(double (&jr)[NN], double& jrd, double (&z)[NN],
-                                                      double (&kr)[NN], double& krd,
-                                                      double (&y)[NN]) {
-  const int i = tlane();
-  sfor<0, NN>([&](auto R) {
-    constexpr int r = HD_K(R);
-    double t = (double)(i == r);
-    double u = t;
-    sfor<0, r>([&](auto K) {
-      t = fma(-bc<r>(jr[HD_K(K)]), z[HD_K(K)], t);
-      u = fma(-bc<r>(kr[HD_K(K)]), y[HD_K(K)], u);
-    });
-    z[r] = t * bc<r>(jrd);
-    y[r] = u * bc<r>(krd);
-    pin<NN>(jr);
-    pin(jrd);
-    pin<NN>(kr);
-    pin(krd);
-  });
-}
-
 // lane i of each team: (X x)_i for X's row i (xr) and x distributed over the team
 template <int NN>
 __device__ __forceinline__ double team_matvec(const double (&xr)[NN], double x) {

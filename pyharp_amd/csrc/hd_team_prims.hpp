@@ -164,55 +164,6 @@ __device__ __forceinline__ bool team_chol(double (&a)[NN], double (&lt)[NN], dou
   return ok != 0;
 }
 
-// Two independent Cholesky factorisations in lockstep (a with lt = rows of L^T if
-// WANT_LT, b without): each step's chain -- pivot broadcast, rsq, column scale --
-// is a few dependent instructions, so at two waves per SIMD one factorisation
-// leaves the VALU idle most of the time; two interleaved fill each other's gaps.
-// ok_a / ok_b: no non-positive pivot in a / b.
-template <int NN, bool WANT_LT>
-__device__ __forceinline__ void team_chol2(double (&a)[NN], double (&lt)[NN], double& rda,
-                                           double (&b)[NN], double& rdb, bool& ok_a,
-                                           bool& ok_b) {
-  const int i = tlane();
-  int oka = 1, okb = 1;
-  rda = rdb = 0.0;
-  if constexpr (WANT_LT) sfor<0, NN>([&](auto J) { lt[HD_K(J)] = 0.0; });
-  sfor<0, NN>([&](auto K) {
-    constexpr int k = HD_K(K);
-    double da = bc<k>(a[k]);
-    double db = bc<k>(b[k]);
-    oka &= da > 0.0 ? 1 : 0;
-    okb &= db > 0.0 ? 1 : 0;
-    asm volatile("" : "+v"(oka), "+v"(okb));
-    da = da > 1.0e-300 ? da : 1.0e-300;
-    db = db > 1.0e-300 ? db : 1.0e-300;
-    const double ra = rsq_nr(da), rb = rsq_nr(db);
-    const double lkk = da * ra;
-    const double aik = a[k] * ra, bik = b[k] * rb;
-    a[k] = i >= k ? aik : 0.0;
-    b[k] = i >= k ? bik : 0.0;
-    if (i == k) {
-      rda = ra;
-      rdb = rb;
-    }
-    if constexpr (WANT_LT) {
-      if (i == k) lt[k] = lkk;
-    }
-    sfor<k + 1, NN>([&](auto J) {
-      constexpr int j = HD_K(J);
-      const double ljk = bc<j>(a[k]);
-      const double mjk = bc<j>(b[k]);
-      a[j] = fma(-a[k], ljk, a[j]);
-      b[j] = fma(-b[k], mjk, b[j]);
-      if constexpr (WANT_LT) {
-        if (i == k) lt[j] = ljk;
-      }
-    });
-  });
-  ok_a = oka != 0;
-  ok_b = okb != 0;
-}
-
 // x <- L^-1 x  (x distributed: lane i holds x_i)
 template <int NN>
 __device__ __forceinline__ void team_lsolve(const double (&l)[NN], double rd, double& x) {
