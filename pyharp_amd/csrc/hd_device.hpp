@@ -32,6 +32,10 @@ constexpr double kDither = 4.712160915387242e-08;
 // caller's side before calling cdisort (rt_solver_disort.cpp_:80); a caller that
 // wants that convention clamps its umu0 array itself.
 
+// relative distance of an eigenvalue k^2 from the beam resonance 1/mu0^2 within which
+// the layer kernels run jacobi_os_polish
+constexpr double kResPolish = 3.0e-4;
+
 // per-thread status bits (mirrors include/hdisort.h)
 constexpr int kStBadInput = 0x01;
 constexpr int kStEigen = 0x02;
@@ -363,7 +367,7 @@ HD_UNROLL_NN
 // by -/+ t (b_p.b_q) -- the two-sided Jacobi diagonal update, exact at the exact
 // angle and stationary in t there, so the FP32 angle's error only enters at second
 // order; the norms are recomputed from the columns at every sweep start anyway.
-template <int NN>
+template <int NN, bool F64 = false>
 __device__ __forceinline__ void jacobi_os_round(int r, double (&b)[NN][NN], double (&nrm)[NN],
                                                 double (&sg)[NN], double (&rs)[NN], bool on,
                                                 double& off) {
@@ -387,24 +391,27 @@ HD_UNROLL_NN
     off += g2;
     const bool rot = on && g2 > 1.0e-30 * (app * aqq);
     const double d = aqq - app;
-#if HD_JACOBI_F32_ANGLE
-    // The angle in FP32, t = tan(theta) = sgn(d) 2 g / (|d| + sqrt(d^2 + 4 g^2));
-    // c = 1/sqrt(1 + t^2) in FP64, so the rotation is orthogonal to FP64 rounding
-    // whatever t is: an angle good to ~1e-7 only leaves ~1e-7 of g behind, which
-    // the next sweep removes (quadratic convergence until off ~ 1e-7 of the
-    // diagonal; the stop rule sits at 1e-8)
-    const float df = (float)d, g2f = 2.0f * (float)gam;
-    const float wf = __builtin_amdgcn_sqrtf(__builtin_fmaf(g2f, g2f, df * df));
-    const float tf = (df < 0.0f ? -g2f : g2f) * __builtin_amdgcn_rcpf(__builtin_fabsf(df) + wf);
-    const double t = rot ? (double)tf : 0.0;
-#else
-    // w = sqrt(d^2 + 4 g^2): t = sgn(d) 2 g / (|d| + w)
-    const double w2 = rot ? fma(d, d, 4.0 * g2) : 1.0;
-    const double w = w2 * rsq_nr1(w2);
-    const double t = rot ? (d < 0.0 ? -2.0 : 2.0) * gam * rcp_nr(fabs(d) + w) : 0.0;
-#endif
+    double t;
+    if constexpr (HD_JACOBI_F32_ANGLE && !F64) {
+      // The angle in FP32, t = tan(theta) = sgn(d) 2 g / (|d| + sqrt(d^2 + 4 g^2));
+      // c = 1/sqrt(1 + t^2) in FP64, so the rotation is orthogonal to FP64 rounding
+      // whatever t is: an angle good to ~1e-7 only leaves ~1e-7 of g behind, which
+      // the next sweep removes (quadratic convergence until off ~ 1e-7 of the
+      // diagonal; the stop rule sits at 1e-8)
+      const float df = (float)d, g2f = 2.0f * (float)gam;
+      const float wf = __builtin_amdgcn_sqrtf(__builtin_fmaf(g2f, g2f, df * df));
+      const float tf = (df < 0.0f ? -g2f : g2f) * __builtin_amdgcn_rcpf(__builtin_fabsf(df) + wf);
+      t = rot ? (double)tf : 0.0;
+    } else {
+      // w = sqrt(d^2 + 4 g^2): t = sgn(d) 2 g / (|d| + w)
+      const double w2 = rot ? fma(d, d, 4.0 * g2) : 1.0;
+      const double w = w2 * rsq_nr(w2);
+      t = rot ? (d < 0.0 ? -2.0 : 2.0) * gam * rcp_nr(fabs(d) + w) : 0.0;
+    }
     tt[k] = t;
-    cc[k] = rsq_nr1(fma(t, t, 1.0));  // exactly 1 for t = 0
+    // exactly 1 for t = 0.  The column scales accumulate one factor c per rotation;
+    // the polish sweep (jacobi_os_polish) takes c to the last bit
+    cc[k] = F64 ? rsq_nr(fma(t, t, 1.0)) : rsq_nr1(fma(t, t, 1.0));
     gg[k] = gam;
   }
 HD_UNROLL_NN
@@ -469,6 +476,52 @@ HD_UNROLL_NN
       for (int i = 0; i < NN; ++i) b[i][j] *= sg[j];
   }
   return !on;
+}
+
+// One more sweep with the angles in FP64 for the lanes that ask (need): the FP32
+// angles of jacobi_os leave up to ~1e-7 of each pair's coupling at its last sweep --
+// for pairs of small columns of a graded B that is ~1e-13 of their eigenvectors,
+// below anything the fluxes see, except where the beam's particular solution divides
+// by 1/mu0^2 - k^2: within 3e-4 of that resonance the layer kernels polish
+// (profiles/r06/resonance.txt: a C4 layer at 2.3e-6 of it gave 8.7e-7 in the fluxes
+// without the polish, 3e-9 with FP64 angles).  No-op for the other lanes; the wave
+// skips it when no lane needs it.
+template <int NN>
+__device__ __forceinline__ void jacobi_os_polish(double (&b)[NN][NN], bool need) {
+  if constexpr (NN > 1) {
+    if (!__any(need)) return;
+    constexpr int P = NN + (NN & 1);
+    double sg[NN], rs[NN], nrm[NN], off = 0.0;
+HD_UNROLL_NN
+    for (int j = 0; j < NN; ++j) {
+      sg[j] = rs[j] = 1.0;
+      double t = 0.0;
+HD_UNROLL_NN
+      for (int i = 0; i < NN; ++i) t = fma(b[i][j], b[i][j], t);
+      nrm[j] = t;
+    }
+HD_UNROLL_NN
+    for (int r = 0; r < P - 1; ++r) jacobi_os_round<NN, true>(r, b, nrm, sg, rs, need, off);
+HD_UNROLL_NN
+    for (int j = 0; j < NN; ++j)
+HD_UNROLL_NN
+      for (int i = 0; i < NN; ++i) b[i][j] *= sg[j];
+  }
+}
+
+// true when some eigenvalue k^2 = |b_j|^2 of the rotated B lies within `tol` (relative)
+// of the beam resonance k^2 = r2 = 1/mu0^2
+template <int NN>
+__device__ __forceinline__ bool near_resonance(const double (&b)[NN][NN], double r2, double tol) {
+  bool near = false;
+HD_UNROLL_NN
+  for (int j = 0; j < NN; ++j) {
+    double k2 = 0.0;
+HD_UNROLL_NN
+    for (int i = 0; i < NN; ++i) k2 = fma(b[i][j], b[i][j], k2);
+    near = near || fabs(r2 - k2) < tol * r2;
+  }
+  return near;
 }
 
 }  // namespace hd

@@ -345,6 +345,7 @@ __device__ __forceinline__ int layer_body(const LayerArgs& A, long s, int sl, in
   asm volatile("" ::: "memory");
   HD_PHASE();
   if (!jacobi_os<NN>(v, A.max_sweeps)) st |= kStEigen;
+  jacobi_os_polish<NN>(v, beam && near_resonance<NN>(v, rmu0 * rmu0, kResPolish));
   HD_PHASE();
   double kk[NN], rk[NN];  // k_j = |b_j|, 1/k_j
 #pragma unroll

@@ -355,8 +355,7 @@ HD_RUNROLL
       y2[i] = Qc.g[i] * rv;
       lxd[i] = Qc.sd[i] * xdi;
     }
-    lower_solve<NN>(lch, rdl, y2);
-    lower_t_solve<NN>(lch, rdl, y2);  // L^-T y2: V^T y2 = U^T L^-T y2 below
+    lower_solve<NN>(lch, rdl, y2);  // V^T y2 below
     lower_solve<NN>(lch, rdl, lxd);
     lower_t_solve<NN>(lch, rdl, lxd);
   } else {
@@ -402,22 +401,23 @@ HD_RUNROLL
       for (int k = 0; k <= i; ++k) rec_st<kRadNt>(&rr[(e++) * nu], lch[i][k]);
   }
 
-  // ---- eigenpairs (hd_layer_kernel's form): C C^T = -A+, Sym = B^T B for
-  // B = C^T L; the one-sided Jacobi gives k^2 = |b_j|^2 and B = B0 V, so
-  // U = L V = C^-T B; V = L^-1 U is stored for the later kernels ----
+  // ---- eigenpairs (hd_layer_kernel's form): C C^T = -A+, X = L^T C, Sym = X X^T;
+  // the one-sided Jacobi on X's columns gives B = X W with k_j = |b_j| and
+  // V = B K^-1 (stored for the later kernels), U = L V ----
   double rdc[NN];
   if (!chol_inplace<NN>(ap, rdc)) st |= kStEigen;  // lower ap <- C
-  double v[NN][NN];  // B, then U = L V, then Omega = U Delta^1/2
+  double v[NN][NN];  // X, then B, then V, then Omega = L V Delta^1/2
 HD_RUNROLL
   for (int i = 0; i < NN; ++i)
 HD_RUNROLL
-    for (int j = 0; j < NN; ++j) {  // B_ij = sum_{k >= max(i,j)} C_ki L_kj
+    for (int j = 0; j < NN; ++j) {  // X_ij = sum_{k >= max(i,j)} L_ki C_kj
       double t = 0.0;
 HD_RUNROLL
-      for (int k = (i > j ? i : j); k < NN; ++k) t = fma(ap[k][i], lch[k][j], t);
+      for (int k = (i > j ? i : j); k < NN; ++k) t = fma(lch[k][i], ap[k][j], t);
       v[i][j] = t;
     }
   if (!jacobi_os<NN>(v, A.max_sweeps)) st |= kStEigen;
+  jacobi_os_polish<NN>(v, beam && near_resonance<NN>(v, rmu0 * rmu0, kResPolish));
   double kk[NN];
 HD_RUNROLL
   for (int j = 0; j < NN; ++j) {
@@ -425,17 +425,11 @@ HD_RUNROLL
 HD_RUNROLL
     for (int i = 0; i < NN; ++i) k2 = fma(v[i][j], v[i][j], k2);
     if (!(k2 > 0.0)) st |= kStEigen;
-    kk[j] = sqrt(k2 > 0.0 ? k2 : 0.0);
+    const double rk = k2 > 0.0 ? rsq_nr(k2) : 0.0;
+    kk[j] = k2 * rk;
     rec_st<kRadNt>(&rr[(oK + j) * nu], kk[j]);
-  }
 HD_RUNROLL
-  for (int j = 0; j < NN; ++j) {  // U = C^-T B, column by column
-    double x[NN];
-HD_RUNROLL
-    for (int i = 0; i < NN; ++i) x[i] = v[i][j];
-    lower_t_solve<NN>(ap, rdc, x);
-HD_RUNROLL
-    for (int i = 0; i < NN; ++i) v[i][j] = x[i];
+    for (int i = 0; i < NN; ++i) v[i][j] *= rk;  // V = B K^-1
   }
 
   // ---- beam particular solution at the layer top ----
@@ -445,7 +439,7 @@ HD_RUNROLL
     double tt[NN];
     const double r2 = rmu0 * rmu0;
 HD_RUNROLL
-    for (int j = 0; j < NN; ++j) {  // tt = V^T y2 / (1/mu0^2 - k^2), V^T y2 = U^T (L^-T y2)
+    for (int j = 0; j < NN; ++j) {  // tt = V^T y2 / (1/mu0^2 - k^2)
       double t = 0.0;
 HD_RUNROLL
       for (int i = 0; i < NN; ++i) t = fma(v[i][j], y2[i], t);
@@ -458,10 +452,17 @@ HD_RUNROLL
     }
     double sv[NN], y[NN];
 HD_RUNROLL
-    for (int i = 0; i < NN; ++i) {  // s = W^-1 D^1/2 L V tt = W^-1 D^1/2 U tt
+    for (int i = 0; i < NN; ++i) {  // V tt
       double t = 0.0;
 HD_RUNROLL
       for (int j = 0; j < NN; ++j) t = fma(v[i][j], tt[j], t);
+      y[i] = t;
+    }
+HD_RUNROLL
+    for (int i = NN - 1; i >= 0; --i) {  // s = W^-1 D^1/2 L V tt
+      double t = 0.0;
+HD_RUNROLL
+      for (int k = 0; k <= i; ++k) t = fma(lch[i][k], y[k], t);
       sv[i] = Qc.rg[i] * t;
     }
 HD_RUNROLL
@@ -501,21 +502,30 @@ HD_RUNROLL
   }
   rec_st<kRadNt>(&rr[oE0 * nu], e0);
 HD_RUNROLL
-  for (int j = 0; j < NN; ++j) {  // V = L^-1 U (stored), Psi^T = L^-T V Gamma^1/2 -> LDS
+  for (int j = 0; j < NN; ++j) {  // V (stored), Psi^T = L^-T V Gamma^1/2 -> LDS
     double x[NN];
 HD_RUNROLL
-    for (int i = 0; i < NN; ++i) x[i] = v[i][j];
-    lower_solve<NN>(lch, rdl, x);
-HD_RUNROLL
-    for (int i = 0; i < NN; ++i) rec_st<kRadNt>(&rr[(oV + i * NN + j) * nu], x[i]);
+    for (int i = 0; i < NN; ++i) {
+      rec_st<kRadNt>(&rr[(oV + i * NN + j) * nu], v[i][j]);
+      x[i] = v[i][j] * gsq[j];
+    }
     lower_t_solve<NN>(lch, rdl, x);
 HD_RUNROLL
-    for (int i = 0; i < NN; ++i) psi_at(i * NN + j) = x[i] * gsq[j];
+    for (int i = 0; i < NN; ++i) psi_at(i * NN + j) = x[i];
   }
 HD_RUNROLL
-  for (int i = 0; i < NN; ++i)  // Omega = L V Delta^1/2 = U Delta^1/2
+  for (int j = 0; j < NN; ++j)  // Omega = L V Delta^1/2, in place (rows bottom-up)
 HD_RUNROLL
-    for (int j = 0; j < NN; ++j) v[i][j] *= dsq[j];
+    for (int i = 0; i < NN; ++i) v[i][j] *= dsq[j];
+HD_RUNROLL
+  for (int i = NN - 1; i >= 0; --i)
+HD_RUNROLL
+    for (int j = 0; j < NN; ++j) {
+      double t = 0.0;
+HD_RUNROLL
+      for (int k = 0; k <= i; ++k) t = fma(lch[i][k], v[k][j], t);
+      v[i][j] = t;
+    }
 
   double* out = A.rsw + (size_t)lc * ne1<NN>() * nu + u;
   double ga[NN], gb[NN];

@@ -281,7 +281,9 @@ __device__ __forceinline__ void team_jacobi_round(double (&b)[NN], double& own, 
   const float wf = __builtin_amdgcn_sqrtf(__builtin_fmaf(g2f, g2f, df * df));
   const float tf = (df < 0.0f ? -g2f : g2f) * __builtin_amdgcn_rcpf(__builtin_fabsf(df) + wf);
   const double t = r ? (double)tf : 0.0;
-  const double c = rsq_nr1(fma(t, t, 1.0));  // exactly 1 for t = 0
+  // c to the last bit: with HD_JACOBI_SCALED the column scale accumulates c
+  // (jacobi_os_round)
+  const double c = rsq_nr(fma(t, t, 1.0));  // exactly 1 for t = 0
   const double s = t * c;
 #else
   // w = sqrt(d^2 + 4 g^2), u = |d| + w, z = 1/sqrt(2 w u): c = u z, s = sgn(d) 2 g z
