@@ -23,15 +23,21 @@ ctx = _context(0)
 ctx.set_chunk(W * C)
 out = d.forward(prop, bc)
 torch.cuda.synchronize()
+sweeps = int(os.environ.get("HD_MAX_SWEEPS", "0"))
+if sweeps:  # debug cap on the Jacobi sweeps (the results are then not converged)
+    ctx.set_max_sweeps(sweeps)
 lay, swp = [], []
 for _ in range(5):
     ctx.set_timing(True)
-    out = d.forward(prop, bc)
+    try:
+        out = d.forward(prop, bc)
+    except RuntimeError:  # capped sweeps flag HD_STATUS_EIGEN
+        pass
     torch.cuda.synchronize()
     tm = ctx.timing()
     lay.append(tm.layer_ms)
     swp.append(tm.sweep_ms)
 lay.sort()
 swp.sort()
-print(f"{sys.argv[1] if len(sys.argv) > 1 else 'cur'}: layer alone {lay[2]:.3f} ms (min {lay[0]:.3f}), "
+print(f"{sys.argv[1] if len(sys.argv) > 1 else 'cur'} (max sweeps {sweeps or 'default'}): layer alone {lay[2]:.3f} ms (min {lay[0]:.3f}), "
       f"sweep+backsub {swp[2]:.3f} ms, checksum {float(out.sum()):.12e}")
