@@ -274,16 +274,27 @@ __global__ __launch_bounds__(64, 2) void hd_team_mfma_layer_kernel(LayerArgs A) 
   const double mub = beam ? mu0 : 0.0;
 
   // ---- phase-matrix rows: S+ = -A+ (ap), S- = -A- (lch); beam source sums ----
+  // chi_1 .. chi_{N-1} of the team's record staged in LDS (the G area, free until the
+  // eigenvalues): lane i of team t loads chi_{i+1} and chi_{i+17}, one round trip for the
+  // whole record instead of one per iteration of the loop below
+  {
+    double* gm = G + t * 32;
+    const int l1 = i + 1, l2 = i + 1 + 16;
+    gm[i] = (l1 < N && l1 <= nm) ? q[1 + l1] : 0.0;
+    gm[16 + i] = (l2 < N && l2 <= nm) ? q[1 + l2] : 0.0;
+    lds_fence();
+  }
   double ap[NN], lch[NN];
   double xs = 0.0, xd = 0.0;
   sfor<0, NN>([&](auto J) { ap[HD_K(J)] = lch[HD_K(J)] = 0.0; });
   {
     double pprev = 0.0, pcur = 1.0;
+    const double* gm = G + t * 32 - 1;  // gm[l] = chi_l
 #pragma nounroll
     for (int l2 = 0; l2 < NN; ++l2) {
       const int le = 2 * l2, lo = le + 1;
-      const double che = le == 0 ? 1.0 : (le <= nm ? q[1 + le] : 0.0);
-      const double cho = lo <= nm ? q[1 + lo] : 0.0;
+      const double che = le == 0 ? 1.0 : gm[le];
+      const double cho = gm[lo];
       const double ge = (2 * le + 1) * (che - f) * rf;
       const double go = (2 * lo + 1) * (cho - f) * rf;
       const double pe0 = pcur;

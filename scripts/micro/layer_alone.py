@@ -14,8 +14,14 @@ from pyharp_amd import Disort, DisortOptions  # noqa: E402
 from pyharp_amd.disort import _context  # noqa: E402
 
 dev = torch.device("cuda", 0)
-W, C, L, nstr = 4, 8192, 80, 16
-prop, bc, _ = bench.make_inputs(list(range(W)), C, L, nstr, False, dev)
+nstr = int(os.environ.get("LAYER_NSTR", "16"))
+if nstr > 16:  # C5-like team-path chunk (16 384 solves)
+    W, C, L = 4, 4096, 80
+    prop, bc, _ = bench.make_inputs(list(range(W)), C, L, nstr, False, dev, ssa=(0.9, 0.9999),
+                                    gasym=(0.6, 0.9), umu0=(0.1, 1.0))
+else:
+    W, C, L = 4, 8192, 80
+    prop, bc, _ = bench.make_inputs(list(range(W)), C, L, nstr, False, dev)
 op = DisortOptions().flags("lamber,quiet,onlyfl").nwave(W).ncol(C)
 op.ds().nlyr, op.ds().nstr, op.ds().nmom = L, nstr, nstr
 d = Disort(op)

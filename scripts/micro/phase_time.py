@@ -21,9 +21,20 @@ NAMES = ["", "assembly (loads, Legendre)", "chol L + beam vectors", "Planck vect
          "beam part 1 + L reload", "beam part 2", "Delta^1/2 (expm1)", "Psi^T -> LDS",
          "Omega = L B K^-1 D^1/2", "A- (Gram, chol, inverse)", "A+ (LDS, Gram, chol, inverse)",
          "stores R~ T~ S~", "  first loads (tau, ssa, f)", "  umu0, fbeam", "  Legendre loop"]
+TEAM = ["", "assembly (loads, Legendre)", "chol S- (L)", "beam vectors", "Planck, L^-T",
+        "chol S+ (C), B0", "warm start (MFMA), C^-T", "Jacobi", "k, Delta, Gamma",
+        "MFMA W, U, U^T", "beam", "Psi, Omega, Grams (MFMA)", "A- (chol, inverse, MFMA)",
+        "A+ (chol, inverse, MFMA)", "", "stores R~ T~ S~", "", "", ""]
 dev = torch.device("cuda", 0)
-W, C, L, nstr = 4, 8192, 80, 16
-prop, bc, _ = bench.make_inputs(list(range(W)), C, L, nstr, False, dev)
+nstr = int(os.environ.get("PHASE_NSTR", "16"))
+if nstr > 16:  # C5-like: one 16 384-solve chunk of the team path
+    NAMES = TEAM
+    W, C, L = 4, 4096, 80
+    prop, bc, _ = bench.make_inputs(list(range(W)), C, L, nstr, False, dev, ssa=(0.9, 0.9999),
+                                    gasym=(0.6, 0.9), umu0=(0.1, 1.0))
+else:
+    W, C, L = 4, 8192, 80
+    prop, bc, _ = bench.make_inputs(list(range(W)), C, L, nstr, False, dev)
 op = DisortOptions().flags("lamber,quiet,onlyfl").nwave(W).ncol(C)
 op.ds().nlyr, op.ds().nstr, op.ds().nmom = L, nstr, nstr
 d = Disort(op)
@@ -37,9 +48,9 @@ lib.hd_debug_phase(buf, 1)
 d.forward(prop, bc)
 torch.cuda.synchronize()
 lib.hd_debug_phase(buf, 1)
-waves = W * C * L // 64
+waves = W * C * L // (64 if nstr <= 16 else 4)
 tot = sum(buf[k] for k in range(1, 19))
 print(f"{waves} waves; cycles per wave by phase (s_memtime):")
-for k in list(range(1, 16)) + [16, 17, 18]:
+for k in [k for k in list(range(1, 16)) + [16, 17, 18] if k < len(NAMES) and NAMES[k]]:
     print(f"  {k:2d} {NAMES[k]:32s} {buf[k] / waves:9.0f}  {100.0 * buf[k] / tot:5.1f} %")
 print(f"  total {tot / waves:.0f}")
