@@ -26,8 +26,11 @@ def main():
         raise SystemExit(f"{kern} not in {sys.argv[2]}")
     r = rows[0]
     calls, avg = int(r["Calls"]), float(r["AverageNs"]) * 1e-9
-    launches_per_step = round(calls / (line["steps"] + line["warmup"] + 1))
-    per_launch = solves / launches_per_step
+    # solves per launch from the line itself (achieved x its average launch / FLOP per
+    # solve): the stats file also holds the launches of the line's extra legs
+    # (unfused, end-to-end), so calls / steps does not give it
+    per_launch = round(rf["achieved"] * 1e12 * rf["avg_launch_ms"] * 1e-3 / rf["flop_per_solve"])
+    launches_per_step = round(solves / per_launch)
     frac = rf["flop_per_solve"] * per_launch / avg / PEAK
     print(f"{r['Name']}: {calls} launches, trace average {avg * 1e3:.3f} ms "
           f"({launches_per_step} per step, {per_launch:.0f} solves each)")
