@@ -74,6 +74,12 @@ __device__ __forceinline__ const Quad<NN>& quad_opaque() {
 // one wave per block: a layer-kernel wave can take any SIMD the previous chunk's
 // sweep leaves free (hd_solve runs the two on separate streams)
 constexpr int kLayerBlock = 64;
+// The layer kernel warms L2 with the prop record of the block dispatched this many blocks
+// later (same XCD; 0: off).  Swept on the GPU, profiles/r06/layer_prefetch_ab.txt: layer
+// kernel alone 1.70 -> 1.60-1.65 ms; C4 +0.7 %, the 8-GPU rank shape +4 % at 384.
+#ifndef HD_LAYER_PREFETCH
+#define HD_LAYER_PREFETCH 384
+#endif
 constexpr int kLayersPerBlock = kLayerBlock / 64;
 
 // phase boundary: keeps the scheduler from hoisting the next phase's loads
@@ -167,7 +173,8 @@ struct ColRec {
 // OPQ: the quadrature table through quad_opaque (the column kernel's layer loop)
 template <int NN, bool OPQ, class Out>
 __device__ __forceinline__ int layer_body(const LayerArgs& A, long s, int sl, int lc,
-                                          double* psi_lds, int lt, Out& out) {
+                                          double* psi_lds, int lt, Out& out,
+                                          const double* pf = nullptr, float* pf_sink = nullptr) {
   constexpr int N = 2 * NN;
   constexpr int kPsi = psi_doubles<NN>();
   const Quad<NN>& Qc = OPQ ? quad_opaque<NN>() : quad<NN>();
@@ -343,6 +350,21 @@ __device__ __forceinline__ int layer_body(const LayerArgs& A, long s, int sl, in
     }
   }
   asm volatile("" ::: "memory");
+#if HD_LAYER_PREFETCH
+  // warm L2 with the record of the block dispatched HD_LAYER_PREFETCH blocks later (same
+  // XCD): three LDS-DMA dword loads touch the lines of its (2 + nmom)-double record (144
+  // bytes at C4; longer records are touched at their first 144 bytes); the data lands in
+  // a sink nobody reads.  Issued here, after this layer's own loads are consumed
+  // and L is parked, so the Jacobi's ~36 k cycles of pure VALU cover the round trip.
+  if (pf) {
+    using gp = const __attribute__((address_space(1))) void*;
+    using lp = __attribute__((address_space(3))) void*;
+    const int o1 = np > 16 ? 16 : np - 1, o2 = np > 17 ? 17 : np - 1;  // inside the record
+    __builtin_amdgcn_global_load_lds((gp)(pf), (lp)(pf_sink), 4, 0, 0);
+    __builtin_amdgcn_global_load_lds((gp)(pf + o1), (lp)(pf_sink), 4, 0, 0);
+    __builtin_amdgcn_global_load_lds((gp)(pf + o2), (lp)(pf_sink), 4, 0, 0);
+  }
+#endif
   HD_PHASE();
   if (!jacobi_os<NN>(v, A.max_sweeps)) st |= kStEigen;
   jacobi_os_polish<NN>(v, beam && near_resonance<NN>(v, rmu0 * rmu0, kResPolish));
@@ -590,21 +612,39 @@ __global__ __launch_bounds__(kLayerBlock) void hd_layer_kernel(LayerArgs A) {
   // reader of a line finds it in L2 instead of HBM
   const int lt = threadIdx.x;
   const int ntl = (A.nlyr + kLayersPerBlock - 1) / kLayersPerBlock;
-  int ts, tl;
-  {
-    const int nb = (int)gridDim.x, b = (int)blockIdx.x;
+  const int nb = (int)gridDim.x;
+  auto tile_of = [&](int b, int& ts, int& tl) {
     const int x = b & 7, base = nb >> 3, extra = nb & 7;
     const int logical = x * base + (x < extra ? x : extra) + (b >> 3);
     ts = logical / ntl;
     tl = logical - ts * ntl;
-  }
+  };
+  int ts, tl;
+  tile_of((int)blockIdx.x, ts, tl);
   const int sl = ts * 64 + (lt & 63);
   const int lc = tl * kLayersPerBlock + (lt >> 6);  // solver layer, 0 = top
   if (sl >= A.nsc || lc >= A.nlyr) return;
   const long s = solve_of(A.s0 + sl, A.cmaj, A.nwave, A.ncol);
   PairOutT<NT> out{reinterpret_cast<double2*>(A.scr) + (size_t)lc * RecL<NN>::pairs * A.nsc + sl,
                    (size_t)A.nsc, 0.0};
+#if HD_LAYER_PREFETCH
+  __shared__ float pf_sink[kLayerBlock];
+  const double* pf = nullptr;
+  if ((int)blockIdx.x + HD_LAYER_PREFETCH < nb) {
+    int ts2, tl2;
+    tile_of((int)blockIdx.x + HD_LAYER_PREFETCH, ts2, tl2);
+    int sl2 = ts2 * 64 + (lt & 63);
+    const int lc2 = tl2 * kLayersPerBlock + (lt >> 6);
+    if (sl2 >= A.nsc) sl2 = A.nsc - 1;
+    if (lc2 < A.nlyr) {
+      const long s2 = solve_of(A.s0 + sl2, A.cmaj, A.nwave, A.ncol);
+      pf = A.prop + ((size_t)s2 * A.nlyr + (A.nlyr - 1 - lc2)) * A.nprop;
+    }
+  }
+  const int st = layer_body<NN, false>(A, s, sl, lc, psi_lds, lt, out, pf, pf_sink);
+#else
   const int st = layer_body<NN, false>(A, s, sl, lc, psi_lds, lt, out);
+#endif
   if (st) {
     atomicOr(&A.status[s], st);
     if (st & 0x0F) atomicOr(A.anyerr, 1);
