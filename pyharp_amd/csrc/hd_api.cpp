@@ -28,6 +28,10 @@ struct hd_context {
   int device = 0;
   double* scratch = nullptr;
   size_t scratch_doubles = 0;
+  // per-g fluxes of hd_solve_band's row-major route (band_rowmajor)
+  double* pflux = nullptr;
+  size_t pflux_doubles = 0;
+  int band_cmaj = 0;  // A/B (HD_BAND_CMAJ=1): always the column-major fused epilogue
   int* status = nullptr;  // internal per-solve status (when caller passes NULL)
   size_t status_len = 0;
   int* anyerr = nullptr;
@@ -256,6 +260,17 @@ long auto_chunk(long nsolve, int nn, int nlyr, bool planck) {
 // The largest chunk auto_chunk gives any call of at most nsolve solves (the chunk
 // size is not monotone in nsolve: 163 840 solves run in chunks of 32 768, 80 000 in
 // chunks of 40 000), so hd_context_reserve(nsolve) covers every smaller call too.
+// hd_solve_band without caller fluxes on the register path, when the call runs as the
+// three-stream pipeline of five or more automatic chunks (the 32 768-solve regime): the
+// row-major chunks of hd_solve into a per-g flux buffer of the context, then
+// hd_band_flux.  C4: 14.80-14.92 M solves/s against 14.33-14.45 M for the column-major
+// fused epilogue on one box (profiles/r06/fuse_ab.txt); the 8-GPU rank shape (two
+// chunks) is equal and the small shapes keep the fused epilogue.
+bool band_rowmajor(const hd_context* ctx, int nn, long nsolve) {
+  return nn <= hd::kMaxRegNN && ctx->chunk <= 0 && !ctx->band_cmaj && !ctx->column &&
+         (nsolve + 32767) / 32768 >= 5;
+}
+
 long max_auto_chunk(long nsolve, int nn, int nlyr, bool planck) {
   const long cap = nn <= hd::kMaxRegNN ? kRegChunkMax : team_chunk_target(nn, nlyr, planck);
   return std::min(nsolve, cap);
@@ -286,6 +301,26 @@ int ensure_scratch(hd_context* ctx, size_t ndoubles) {
                 ndoubles * sizeof(double));
   }
   ctx->scratch_doubles = ndoubles;
+  return HD_OK;
+}
+
+int ensure_pflux(hd_context* ctx, size_t ndoubles) {
+  if (ctx->pflux_doubles >= ndoubles) return HD_OK;
+  if (ctx->capturing)
+    return fail(ctx, HD_EINVAL,
+                "hd_solve_band: the per-g flux buffer must grow to %zu bytes inside a stream "
+                "capture; size the context first (hd_context_reserve, or one eager call of the "
+                "same shape)", ndoubles * sizeof(double));
+  drain(ctx);
+  if (ctx->pflux) (void)hipFree(ctx->pflux);
+  ctx->pflux = nullptr;
+  ctx->pflux_doubles = 0;
+  if (hipMalloc(&ctx->pflux, ndoubles * sizeof(double)) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(ctx, HD_ENOMEM, "hd_solve_band: cannot allocate %zu bytes of per-g fluxes",
+                ndoubles * sizeof(double));
+  }
+  ctx->pflux_doubles = ndoubles;
   return HD_OK;
 }
 
@@ -424,6 +459,7 @@ int hd_context_create(hd_context** out, int device) {
   hd_context* ctx = new hd_context();
   if (const char* e = hd::ab_env("HD_JACOBI_WARM")) ctx->warm = std::atoi(e) != 0;
   if (const char* e = hd::ab_env("HD_SWEEP_QUAD")) ctx->quad = std::atoi(e) < 0 ? -1 : std::atoi(e) != 0;
+  if (const char* e = hd::ab_env("HD_BAND_CMAJ")) ctx->band_cmaj = std::atoi(e) != 0;
 #if HD_AB_VARIANTS
   if (const char* e = hd::ab_env("HD_TEAM_SWEEP_LEAN")) ctx->lean = std::atoi(e) != 0;
   if (const char* e = hd::ab_env("HD_SWEEP_LEAN8")) ctx->lean8 = std::atoi(e) != 0;
@@ -466,6 +502,7 @@ int hd_context_destroy(hd_context* ctx) {
   (void)hipSetDevice(ctx->device);
   drain(ctx);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->pflux) (void)hipFree(ctx->pflux);
   if (ctx->hstage) (void)hipFree(ctx->hstage);
   if (ctx->hstream) (void)hipStreamDestroy(ctx->hstream);
   if (ctx->hstream2) (void)hipStreamDestroy(ctx->hstream2);
@@ -549,6 +586,11 @@ int hd_context_reserve(hd_context* ctx, const hd_config* cfg, long nsolve) {
                                      2 * (size_t)c1 * 2 * (size_t)(cfg->nlyr + 1));
   int rc = ensure_scratch(ctx, per * c1 + band_extra);
   if (rc) return rc;
+  // and hd_solve_band's row-major route (largest call that takes it: nsolve itself)
+  if (band_rowmajor(ctx, cfg->nstr / 2, nsolve)) {
+    rc = ensure_pflux(ctx, (size_t)nsolve * 2 * (size_t)(cfg->nlyr + 1));
+    if (rc) return rc;
+  }
   rc = ensure_tables(ctx);
   if (rc) return rc;
   return ensure_status(ctx, (size_t)nsolve);
@@ -965,7 +1007,19 @@ int hd_solve_band(hd_context* ctx, const hd_config* cfg, const hd_inputs* in,
   // flux is optional here: validate against a non-null stand-in
   int rc = validate(ctx, cfg, in, flux ? flux : band->bflux);
   if (rc) return rc;
-  if ((long)in->nwave * in->ncol == 0) return HD_OK;
+  const long nsolve = (long)in->nwave * in->ncol;
+  if (nsolve == 0) return HD_OK;
+  if (!flux && band_rowmajor(ctx, cfg->nstr / 2, nsolve)) {
+    return run_solve(ctx, status, stream, "hd_solve_band", [&](int*& st, hipStream_t s) {
+      int r = ensure_pflux(ctx, (size_t)nsolve * 2 * (size_t)(cfg->nlyr + 1));
+      if (r) return r;
+      r = solve_enqueue(ctx, cfg, in, ctx->pflux, nullptr, st, s);
+      if (r) return r;
+      r = hd_band_flux(ctx->pflux, band->weight, in->nwave, in->ncol, cfg->nlyr + 1,
+                       band->bflux, s);
+      return r ? fail(ctx, r, "hd_solve_band: hd_band_flux launch failed") : HD_OK;
+    });
+  }
   return run_solve(ctx, status, stream, "hd_solve_band", [&](int*& st, hipStream_t s) {
     return solve_enqueue(ctx, cfg, in, flux, band, st, s);
   });

@@ -800,3 +800,65 @@ def test_reserve_covers_smaller_calls():
     if "error" in res:
         raise res["error"]
     assert torch.equal(res["replay"], res["eager"])
+
+
+@pytest.mark.gpu
+def test_band_rowmajor_route(oracle_c):
+    """hd_solve_band without caller fluxes, five or more automatic chunks on the
+    register path (C4's regime): the row-major chunks of hd_solve into the context's
+    per-g flux buffer, then hd_band_flux.  On a fresh context:
+    reserve(N) sizes that buffer (the captured call must not grow it), the replay
+    equals the eager call bit for bit, and both equal forward + band_flux bit for bit
+    (the same kernels on the same chunks)."""
+    import threading
+    from pyharp_amd import _lib
+    from pyharp_amd.disort import _context
+    from pyharp_amd.spectral import band_flux
+    rng = np.random.default_rng(62)
+    nstr, nwave, ncol, nlyr = 4, 32, 6000, 3
+    cfg = _lib.HdConfig(nstr=nstr, nmom=nstr, nlyr=nlyr, nprop=2 + nstr,
+                        flags=_lib.HD_FLAG_LAMBER | _lib.HD_FLAG_ONLYFL)
+    assert _lib.chunk_solves(nstr, nlyr, nwave * ncol) == 32000  # six chunks
+    prop, bc, _ = _random_batch(rng, nwave, ncol, nlyr, nstr, False)
+    dev = torch.device("cuda", 0)
+    p = torch.as_tensor(prop, device=dev)
+    b = {k: torch.as_tensor(v, device=dev) for k, v in bc.items()}
+    w = torch.as_tensor(rng.uniform(0.1, 1.0, nwave), device=dev)
+    res = {}
+
+    def worker():
+        try:
+            _context(0).reserve(cfg, nwave * ncol)
+            d = _disort(nstr, nlyr, nwave, ncol)
+            st = torch.zeros(nwave * ncol, dtype=torch.int32, device=dev)
+            out = torch.empty((ncol, nlyr + 1, 2), dtype=torch.float64, device=dev)
+            s = torch.cuda.Stream(device=dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s):
+                    d.forward_band(p, b, weights=w, out=out, status=st)
+            out.zero_()
+            g.replay()
+            torch.cuda.synchronize()
+            res["replay"] = out.clone()
+            res["eager"] = d.forward_band(p, b, weights=w)
+            res["unfused"] = band_flux(d.forward(p, b), w)
+            torch.cuda.synchronize()
+        except BaseException as e:  # surfaced in the main thread
+            res["error"] = e
+
+    t = threading.Thread(target=worker)
+    t.start()
+    t.join(timeout=100)
+    assert not t.is_alive()
+    if "error" in res:
+        raise res["error"]
+    assert torch.equal(res["replay"], res["eager"])
+    assert torch.equal(res["eager"], res["unfused"])
+    # and the band flux itself against the C oracle on a subsample of columns
+    cols = np.arange(0, ncol, 997)
+    ref = oracle_c.forward(prop[:, cols], {k: v[:, cols] for k, v in bc.items()}, nstr=nstr)
+    want = np.einsum("g,gcld->cld", w.cpu().numpy(), ref)
+    got = res["eager"].cpu().numpy()[cols]
+    assert np.abs(got - want).max() / np.abs(want).max() < 1e-9
