@@ -129,7 +129,8 @@ int hd_context_set_timing(hd_context *ctx, int enable);
 int hd_context_set_max_sweeps(hd_context *ctx, int max_sweeps);
 int hd_context_get_timing(const hd_context *ctx, hd_timing *out);
 /* pre-size scratch for graph capture / steady state: room for hd_solve and for
- * hd_solve_band (any nwave) of up to nsolve solves of this config, and the status
+ * hd_solve_band (any nwave) of up to nsolve solves of this config (with its per-point
+ * flux buffer when nsolve takes hd_solve_band's row-major route), and the status
  * buffer.  A call captured into a HIP graph never allocates: if scratch would
  * have to grow during capture it returns HD_EINVAL instead. */
 int hd_context_reserve(hd_context *ctx, const hd_config *cfg, long nsolve);
@@ -161,7 +162,12 @@ int hd_solve(hd_context *ctx, const hd_config *cfg, const hd_inputs *in, double 
  * formed in the back-substitution epilogue (solves taken column by column,
  * the weighted fluxes of a column summed across lanes), so the per-point
  * fluxes never reach memory; for nstr 18..32 each chunk's fluxes are summed
- * into bflux after the chunk.  The summation order is fixed (deterministic
+ * into bflux after the chunk.  Exception, for nstr <= 16 with flux NULL and
+ * five or more automatic chunks (C4's regime): the solves run in hd_solve's
+ * row-major chunks into a per-point flux buffer of the context (nwave*ncol*
+ * (nlyr+1)*2 doubles, sized by hd_context_reserve too) and hd_band_flux sums
+ * them -- faster there than the column-order epilogue, and bitwise equal to
+ * hd_solve + hd_band_flux.  The summation order is fixed (deterministic
  * for a given shape and chunk size; no atomics).  Heating rates and the
  * spherical correction follow from bflux (hdharp.h) -- after the cross-rank
  * all-reduce when a band's points are sharded over GPUs.
